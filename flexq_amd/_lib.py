@@ -1,0 +1,90 @@
+"""ctypes binding of libflexq_hip.so (the C ABI declared in include/flexq_hip.h).
+
+The library is the product path: there is no CPU or eager fallback.  If the shared object is
+missing, every op raises `FlexQExtensionError` (build it with `python -c "import
+__graft_entry__ as g; g.build()"` or `make -C flexq_amd/csrc`).
+
+torch is imported before the library is loaded so that the HIP runtime torch already mapped
+(soname libamdhip64.so.7) is the one our code object registers with.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libflexq_hip.so")
+
+FQ_OK = 0
+_STATUS = {1: "FQ_ERR_NULL", 2: "FQ_ERR_SHAPE", 3: "FQ_ERR_BITS", 4: "FQ_ERR_WORKSPACE", 5: "FQ_ERR_HIP"}
+
+
+class FlexQExtensionError(RuntimeError):
+    """The HIP extension is missing or failed to load."""
+
+
+class FlexQError(RuntimeError):
+    """A C-ABI entry point returned a non-zero fq_status."""
+
+    def __init__(self, fn, status):
+        super().__init__(f"{fn} failed: {_STATUS.get(status, status)} ({status})")
+        self.status = status
+
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+SZ = ctypes.c_size_t
+
+# name -> (argtypes, restype)   -- mirrors include/flexq_hip.h
+_SIGS = {
+    "fq_version": ([], ctypes.c_char_p),
+    "fq_status_string": ([I], ctypes.c_char_p),
+    "fq_packed_w_bytes": ([I, I], SZ),
+    "fq_gemm_workspace_bytes": ([I, I, I], SZ),
+    "fq_workspace_init": ([P, SZ, P], I),
+    "fq_pack_w6": ([P, I, I, P, P], I),
+    "fq_unpack_w6": ([P, I, I, P, P], I),
+    "fq_quantize_pack_w6": ([P, I, I, P, P, P, P], I),
+    "fq_quantize_act": ([P, I, I, I, P, P, P], I),
+    "fq_gemm_w6ax": ([P, P, P, P, I, I, I, I, P, P, P, SZ, P], I),
+    "fq_linear_w6ax": ([P, I, I, I, I, P, P, P, P, P, P, SZ, P], I),
+    "fq_ref_bit_packing": ([P, P, I, I, I, P], I),
+    "fq_ref_quantize_bit_packing": ([P, P, P, I, I, I, P], I),
+    "fq_import_ref_w": ([P, I, I, P, P], I),
+    "fq_import_ref_x": ([P, P, I, I, I, P, P, P], I),
+    "fq_bmma_scratch_bytes": ([I, I, I], SZ),
+}
+EXPORTED = tuple(_SIGS) + ("fq_bmma_init", "fq_bmma_exec")
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the CDLL.  Raises FlexQExtensionError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FlexQExtensionError(
+            f"{LIB_PATH} not found: the HIP extension is not built (run __graft_entry__.build())")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise FlexQExtensionError(f"failed to load {LIB_PATH}: {e}") from e
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke an fq_status-returning entry point and raise on failure."""
+    rc = getattr(load(), name)(*args)
+    if rc != FQ_OK:
+        raise FlexQError(name, rc)
+
+
+def version():
+    return load().fq_version().decode()

@@ -1,0 +1,428 @@
+// fq_quant.hip -- dynamic activation quantizer, fq6 weight packer and the reference-layout
+// converters for gfx950.  HBM-bound byte work: 16-byte-per-lane coalesced loads, 16-lane
+// (one DPP row) max-reductions, no LDS round trips.
+#include "fq_common.h"
+
+// =============================================================================================
+// Activation quantizer.  One 128-wide group = 16 lanes x 8 fp16 (16 B per lane), so one wave
+// instruction covers 4 groups = 1 KiB.  Groups are enumerated flat over [M][K/128] (row-major,
+// contiguous in memory), so any K % 128 == 0 works without per-row tails.
+// Arithmetic restates e2e .../flexqgemm/src/pack/bit_packing.cu:125-164 exactly:
+//   absmax in fp16 (exact as float), maxv = absmax / (2^(b-1)-1) in fp32, scale = half(maxv),
+//   q = clamp(roundf(float(x) / float(scale)), lo, hi) with CUDA's saturating conversion.
+// Output variants:
+//   MODE 0: xq int8 [M][K] + xs fp16 [K/128][M]          (this build's GEMM input)
+//   MODE 1: reference bit planes [K/128][M/c][b][c][4] + duplicated x_scale (drop-in pack)
+// =============================================================================================
+template <int MODE>
+__global__ __launch_bounds__(256) void fq_quantize_act_kernel(
+    const uint16_t *__restrict__ x, int M, int K, int bits, int8_t *__restrict__ xq,
+    uint16_t *__restrict__ xs, int32_t *__restrict__ planes, uint16_t *__restrict__ xs_dup) {
+    const int G = K / FQ_GROUP;
+    const long T = (long)M * G;  // total groups
+    const int lane = threadIdx.x & 63;
+    const int sub = lane & 15;  // position inside the group
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
+    const float fhi = (float)hi;
+
+    for (long chunk = wave; chunk * 4 < T; chunk += nwaves) {
+        const long gi = chunk * 4 + (lane >> 4);  // flat group index of this lane
+        const bool valid = gi < T;
+        uint4 raw = make_uint4(0, 0, 0, 0);
+        if (valid) raw = *reinterpret_cast<const uint4 *>(x + gi * FQ_GROUP + sub * 8);
+        uint16_t h[8] = {(uint16_t)raw.x, (uint16_t)(raw.x >> 16), (uint16_t)raw.y,
+                         (uint16_t)(raw.y >> 16), (uint16_t)raw.z, (uint16_t)(raw.z >> 16),
+                         (uint16_t)raw.w, (uint16_t)(raw.w >> 16)};
+        float v[8];
+        float mx = -1.0f;  // the reference seeds the fp16 max with -1 (bit_packing.cu:139)
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            v[i] = h2f(h[i]);
+            mx = fmaxf(mx, fabsf(v[i]));  // fmaxf drops a NaN operand, like __hmax
+        }
+        // max over the 16 lanes of the group (xor 8,4,2,1 stays inside a 16-lane DPP row)
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        const float maxv = mx / fhi;  // IEEE fp32 division (no fast-math in this build)
+        const uint16_t sh = f2h(maxv);
+        const float r = h2f(sh);
+        int q[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) q[i] = sat_clamp(round_half_away(v[i] / r), lo, hi);
+
+        const long m = gi / G, g = gi - (gi / G) * G;
+        if (MODE == 0) {
+            if (valid) {
+                uint32_t w0 = (q[0] & 255) | ((q[1] & 255) << 8) | ((q[2] & 255) << 16) |
+                              ((uint32_t)(q[3] & 255) << 24);
+                uint32_t w1 = (q[4] & 255) | ((q[5] & 255) << 8) | ((q[6] & 255) << 16) |
+                              ((uint32_t)(q[7] & 255) << 24);
+                *reinterpret_cast<uint2 *>(xq + gi * FQ_GROUP + sub * 8) = make_uint2(w0, w1);
+                if (sub == 0) xs[g * M + m] = sh;
+            }
+        } else {
+            // Bit planes: word j of a group covers k = 32j..32j+31 with k0 at bit 31
+            // (__brev(__ballot) at bit_packing.cu:109).  Lane sub = 4j+u holds k = 32j+8u+i.
+            const int chunkM = M < 8 ? M : 8;
+            const int u = sub & 3, j = sub >> 2;
+            for (int b = 0; b < bits; b++) {
+                uint32_t byte = 0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) byte |= (uint32_t)((q[i] >> b) & 1) << (7 - i);
+                uint32_t word = byte << (8 * (3 - u));
+                word |= __shfl_xor(word, 1, 64);
+                word |= __shfl_xor(word, 2, 64);
+                if (valid && u == 0) {
+                    long idx = g * ((long)M * bits * 4) + (m / chunkM) * (bits * chunkM * 4) +
+                               b * (chunkM * 4) + (m % chunkM) * 4 + j;
+                    planes[idx] = (int32_t)word;
+                }
+            }
+            if (valid && sub == 0) {
+                const int ld = 2 * ((M + 3) / 4 * 4);  // SCALE_PACKING_A(SCALE_SIZE_X(M))
+                xs_dup[g * ld + 2 * m] = sh;
+                xs_dup[g * ld + 2 * m + 1] = sh;
+            }
+        }
+    }
+}
+
+static int quant_grid(long groups) {
+    long waves = (groups + 3) / 4;
+    long blocks = (waves + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    return (int)(blocks < 1 ? 1 : blocks);
+}
+
+extern "C" fq_status fq_quantize_act(const uint16_t *x, int M, int K, int abits, int8_t *xq,
+                                     uint16_t *xs, fq_stream_t stream) {
+    if (!x || !xq || !xs) return FQ_ERR_NULL;
+    if (M <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    const long groups = (long)M * (K / FQ_GROUP);
+    hipLaunchKernelGGL(fq_quantize_act_kernel<0>, dim3(quant_grid(groups)), dim3(256), 0,
+                       (hipStream_t)stream, x, M, K, abits, xq, xs, nullptr, nullptr);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+extern "C" fq_status fq_ref_quantize_bit_packing(const uint16_t *x, int32_t *packed,
+                                                 uint16_t *x_scale_dup, int M, int K, int bits,
+                                                 fq_stream_t stream) {
+    if (!x || !packed || !x_scale_dup) return FQ_ERR_NULL;
+    if (M <= 0 || K <= 0 || K % FQ_GROUP || (M > 8 && M % 8)) return FQ_ERR_SHAPE;
+    if (bits != 6 && bits != 8) return FQ_ERR_BITS;
+    const long groups = (long)M * (K / FQ_GROUP);
+    hipLaunchKernelGGL(fq_quantize_act_kernel<1>, dim3(quant_grid(groups)), dim3(256), 0,
+                       (hipStream_t)stream, x, M, K, bits, nullptr, nullptr, packed, x_scale_dup);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+// =============================================================================================
+// Reference bit-plane packing of raw b-bit integers (engine/src/pack/bit_packing.cu:76-133).
+// One thread per output word (row, 32-k word, bit); offline / test path.
+// =============================================================================================
+__global__ void fq_ref_bit_packing_kernel(const int32_t *__restrict__ in, int32_t *__restrict__ out,
+                                          int R, int K, int bits) {
+    const long total = (long)R * (K / 32) * bits;
+    const int chunk = R < 8 ? R : 8;
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long)gridDim.x * blockDim.x) {
+        const int b = (int)(t % bits);
+        const long rk = t / bits;
+        const int kt = (int)(rk % (K / 32));
+        const int r = (int)(rk / (K / 32));
+        const int32_t *src = in + (long)r * K + kt * 32;
+        uint32_t word = 0;
+#pragma unroll 8
+        for (int i = 0; i < 32; i++) word |= (((uint32_t)src[i] >> b) & 1u) << (31 - i);
+        const long idx = (long)(kt / 4) * ((long)R * bits * 4) + (r / chunk) * (bits * chunk * 4) +
+                         b * (chunk * 4) + (r % chunk) * 4 + (kt % 4);
+        out[idx] = (int32_t)word;
+    }
+}
+
+extern "C" fq_status fq_ref_bit_packing(const int32_t *in, int32_t *packed, int M, int K, int bits,
+                                        fq_stream_t stream) {
+    if (!in || !packed) return FQ_ERR_NULL;
+    if (M <= 0 || K <= 0 || K % FQ_GROUP || (M > 8 && M % 8)) return FQ_ERR_SHAPE;
+    if (bits < 1 || bits > 8) return FQ_ERR_BITS;
+    const long total = (long)M * (K / 32) * bits;
+    long blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(fq_ref_bit_packing_kernel, dim3((int)blocks), dim3(256), 0,
+                       (hipStream_t)stream, in, packed, M, K, bits);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+// =============================================================================================
+// fq6 weight layout (oracle fqo_pack_fq6):
+//   uint32 [Npad/32][K/128][4 kstep][64 lane][3 word]
+//   lane l, kstep s: column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j (j = 0..15)
+//   byte b of word r = ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3)
+// One thread builds one lane's 12 bytes, so a wave writes one 768-byte contiguous run.
+// =============================================================================================
+__device__ __forceinline__ void fq6_encode(const int v[16], uint32_t out[3]) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            uint32_t byte = (((uint32_t)v[4 * r + b] & 63u) << 2) | (((uint32_t)v[12 + b] >> (2 * r)) & 3u);
+            w |= byte << (8 * b);
+        }
+        out[r] = w;
+    }
+}
+
+__device__ __forceinline__ void fq6_slot(long slot, int G, int &n, int &k0) {
+    // slot = ((t*G + g)*4 + s)*64 + l
+    const int l = (int)(slot & 63);
+    const long tgs = slot >> 6;
+    const int s = (int)(tgs & 3);
+    const long tg = tgs >> 2;
+    const int g = (int)(tg % G);
+    const int t = (int)(tg / G);
+    n = 32 * t + (l & 31);
+    k0 = 128 * g + 32 * s + 16 * (l >> 5);
+}
+
+__global__ void fq_pack_w6_kernel(const int8_t *__restrict__ wq, int N, int K,
+                                  uint32_t *__restrict__ out) {
+    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
+    const long total = (long)NT * G * 4 * 64;
+    for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
+         slot += (long)gridDim.x * blockDim.x) {
+        int n, k0;
+        fq6_slot(slot, G, n, k0);
+        int v[16];
+        if (n < N) {
+            const int4 raw = *reinterpret_cast<const int4 *>(wq + (long)n * K + k0);
+            const int w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = (int)(int8_t)((w[j >> 2] >> (8 * (j & 3))) & 255);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = 0;
+        }
+        uint32_t p[3];
+        fq6_encode(v, p);
+        uint32_t *dst = out + slot * 3;
+        dst[0] = p[0];
+        dst[1] = p[1];
+        dst[2] = p[2];
+    }
+}
+
+__global__ void fq_unpack_w6_kernel(const uint32_t *__restrict__ in, int N, int K,
+                                    int8_t *__restrict__ wq) {
+    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
+    const long total = (long)NT * G * 4 * 64;
+    for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
+         slot += (long)gridDim.x * blockDim.x) {
+        int n, k0;
+        fq6_slot(slot, G, n, k0);
+        if (n >= N) continue;
+        const uint32_t *src = in + slot * 3;
+        v4i o = unpack_fq6(src[0], src[1], src[2]);
+        int4 res;
+        int *rp = reinterpret_cast<int *>(&res);
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            // each byte holds 4*w; arithmetic shift per byte
+            uint32_t x = (uint32_t)o[d], y = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                int8_t w = (int8_t)(x >> (8 * b)) >> 2;
+                y |= ((uint32_t)(uint8_t)w) << (8 * b);
+            }
+            rp[d] = (int)y;
+        }
+        *reinterpret_cast<int4 *>(wq + (long)n * K + k0) = res;
+    }
+}
+
+static int grid_for(long total) {
+    long blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    return (int)(blocks < 1 ? 1 : blocks);
+}
+
+extern "C" size_t fq_packed_w_bytes(int N, int K) {
+    if (N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
+    return (size_t)((N + 31) / 32) * (K / FQ_GROUP) * 3072;
+}
+
+extern "C" fq_status fq_pack_w6(const int8_t *wq, int N, int K, void *w_packed, fq_stream_t stream) {
+    if (!wq || !w_packed) return FQ_ERR_NULL;
+    if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    hipLaunchKernelGGL(fq_pack_w6_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                       wq, N, K, (uint32_t *)w_packed);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+extern "C" fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, fq_stream_t stream) {
+    if (!wq || !w_packed) return FQ_ERR_NULL;
+    if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    hipLaunchKernelGGL(fq_unpack_w6_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       (hipStream_t)stream, (const uint32_t *)w_packed, N, K, wq);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+// ---- fp16 weight -> scales (pass 1) and codes + fq6 (pass 2), engine rounding rule ----------
+__global__ void fq_weight_scale_kernel(const uint16_t *__restrict__ w, int N, int K,
+                                       uint16_t *__restrict__ ws) {
+    // one 16-lane row per (n, g): same reduction as the activation quantizer (bits = 6)
+    const int G = K / FQ_GROUP;
+    const long T = (long)N * G;
+    const int lane = threadIdx.x & 63, sub = lane & 15;
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    for (long chunk = wave; chunk * 4 < T; chunk += nwaves) {
+        const long gi = chunk * 4 + (lane >> 4);
+        const bool valid = gi < T;
+        uint4 raw = make_uint4(0, 0, 0, 0);
+        if (valid) raw = *reinterpret_cast<const uint4 *>(w + gi * FQ_GROUP + sub * 8);
+        const uint32_t d[4] = {raw.x, raw.y, raw.z, raw.w};
+        float mx = -1.0f;
+#pragma unroll
+        for (int i = 0; i < 8; i++) mx = fmaxf(mx, fabsf(h2f((uint16_t)(d[i >> 1] >> (16 * (i & 1))))));
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        if (valid && sub == 0) {
+            const long n = gi / G, g = gi % G;
+            ws[g * N + n] = f2h(mx / 31.0f);
+        }
+    }
+}
+
+__global__ void fq_weight_pack_kernel(const uint16_t *__restrict__ w, const uint16_t *__restrict__ ws,
+                                      int N, int K, uint32_t *__restrict__ out,
+                                      int8_t *__restrict__ wq_out) {
+    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
+    const long total = (long)NT * G * 4 * 64;
+    for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
+         slot += (long)gridDim.x * blockDim.x) {
+        int n, k0;
+        fq6_slot(slot, G, n, k0);
+        int v[16];
+        if (n < N) {
+            const float r = h2f(ws[(long)(k0 / FQ_GROUP) * N + n]);
+            const uint4 *src = reinterpret_cast<const uint4 *>(w + (long)n * K + k0);
+            const uint4 a = src[0], b = src[1];
+            const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                v[j] = sat_clamp(round_half_away(h2f((uint16_t)(d[j >> 1] >> (16 * (j & 1)))) / r), -32, 31);
+            if (wq_out) {
+                uint32_t pk[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    pk[q] = (v[4 * q] & 255) | ((v[4 * q + 1] & 255) << 8) | ((v[4 * q + 2] & 255) << 16) |
+                            ((uint32_t)(v[4 * q + 3] & 255) << 24);
+                *reinterpret_cast<uint4 *>(wq_out + (long)n * K + k0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = 0;
+        }
+        uint32_t p[3];
+        fq6_encode(v, p);
+        uint32_t *dst = out + slot * 3;
+        dst[0] = p[0];
+        dst[1] = p[1];
+        dst[2] = p[2];
+    }
+}
+
+extern "C" fq_status fq_quantize_pack_w6(const uint16_t *w, int N, int K, void *w_packed,
+                                         uint16_t *ws, int8_t *wq_out, fq_stream_t stream) {
+    if (!w || !w_packed || !ws) return FQ_ERR_NULL;
+    if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    hipLaunchKernelGGL(fq_weight_scale_kernel, dim3(quant_grid((long)N * (K / FQ_GROUP))), dim3(256),
+                       0, (hipStream_t)stream, w, N, K, ws);
+    FQ_LAUNCH_CHECK();
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    hipLaunchKernelGGL(fq_weight_pack_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       (hipStream_t)stream, w, ws, N, K, (uint32_t *)w_packed, wq_out);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+// ---- reference bit-plane layout -> this build's layouts ------------------------------------
+__device__ __forceinline__ int bitplane_value(const int32_t *__restrict__ planes, int R, int bits,
+                                              int r, int k) {
+    const int chunk = R < 8 ? R : 8;
+    const int kt = k >> 5;
+    const long base = (long)(kt / 4) * ((long)R * bits * 4) + (r / chunk) * (bits * chunk * 4) +
+                      (r % chunk) * 4 + (kt % 4);
+    int v = 0;
+    for (int b = 0; b < bits; b++) {
+        const int bit = ((uint32_t)planes[base + b * (chunk * 4)] >> (31 - (k & 31))) & 1;
+        v += (b == bits - 1) ? -(bit << b) : (bit << b);
+    }
+    return v;
+}
+
+__global__ void fq_import_ref_w_kernel(const int32_t *__restrict__ planes, int N, int K,
+                                       uint32_t *__restrict__ out) {
+    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
+    const long total = (long)NT * G * 4 * 64;
+    for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
+         slot += (long)gridDim.x * blockDim.x) {
+        int n, k0;
+        fq6_slot(slot, G, n, k0);
+        int v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = (n < N) ? bitplane_value(planes, N, 6, n, k0 + j) : 0;
+        uint32_t p[3];
+        fq6_encode(v, p);
+        uint32_t *dst = out + slot * 3;
+        dst[0] = p[0];
+        dst[1] = p[1];
+        dst[2] = p[2];
+    }
+}
+
+__global__ void fq_import_ref_x_kernel(const int32_t *__restrict__ planes,
+                                       const uint16_t *__restrict__ xs_dup, int M, int K, int bits,
+                                       int8_t *__restrict__ xq, uint16_t *__restrict__ xs) {
+    const long total = (long)M * K;
+    const int ld = 2 * ((M + 3) / 4 * 4);
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long)gridDim.x * blockDim.x) {
+        const int m = (int)(i / K), k = (int)(i % K);
+        xq[i] = (int8_t)bitplane_value(planes, M, bits, m, k);
+        if ((k & (FQ_GROUP - 1)) == 0) xs[(long)(k / FQ_GROUP) * M + m] = xs_dup[(long)(k / FQ_GROUP) * ld + 2 * m];
+    }
+}
+
+extern "C" fq_status fq_import_ref_w(const int32_t *w_bitplanes, int N, int K, void *w_packed,
+                                     fq_stream_t stream) {
+    if (!w_bitplanes || !w_packed) return FQ_ERR_NULL;
+    if (N <= 0 || K <= 0 || K % FQ_GROUP || (N > 8 && N % 8)) return FQ_ERR_SHAPE;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    hipLaunchKernelGGL(fq_import_ref_w_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       (hipStream_t)stream, w_bitplanes, N, K, (uint32_t *)w_packed);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+extern "C" fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, int M,
+                                     int K, int bits, int8_t *xq, uint16_t *xs, fq_stream_t stream) {
+    if (!x_bitplanes || !x_scale_dup || !xq || !xs) return FQ_ERR_NULL;
+    if (M <= 0 || K <= 0 || K % FQ_GROUP || (M > 8 && M % 8)) return FQ_ERR_SHAPE;
+    if (bits != 6 && bits != 8) return FQ_ERR_BITS;
+    hipLaunchKernelGGL(fq_import_ref_x_kernel, dim3(grid_for((long)M * K)), dim3(256), 0,
+                       (hipStream_t)stream, x_bitplanes, x_scale_dup, M, K, bits, xq, xs);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}

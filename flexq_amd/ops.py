@@ -1,0 +1,221 @@
+"""Torch-facing wrappers of the C ABI (include/flexq_hip.h).
+
+Every function validates shapes/dtypes/devices on the host before anything is enqueued, passes
+raw device pointers and torch's current HIP stream to libflexq_hip.so, and returns new tensors.
+There is no fallback: CPU tensors are rejected and a missing library raises.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+GROUP = 128
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _need(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _dev(t, dtype, name, dim=None):
+    _need(isinstance(t, torch.Tensor), f"{name} must be a tensor")
+    _need(t.is_cuda, f"{name} must be a HIP device tensor (no CPU path by design)")
+    _need(t.dtype == dtype, f"{name} must be {dtype}, got {t.dtype}")
+    _need(t.is_contiguous(), f"{name} must be contiguous")
+    if dim is not None:
+        _need(t.dim() == dim, f"{name} must be {dim}-D, got shape {tuple(t.shape)}")
+
+
+def _k_ok(K):
+    _need(K > 0 and K % GROUP == 0, f"K={K} must be a positive multiple of {GROUP}")
+
+
+# ------------------------------------------------------------------------- sizes / workspace
+
+def packed_w_bytes(N, K):
+    return int(_lib.load().fq_packed_w_bytes(N, K))
+
+
+def gemm_workspace_bytes(M, N, K):
+    return int(_lib.load().fq_gemm_workspace_bytes(M, N, K))
+
+
+_WS = {}
+
+
+def workspace(device, nbytes, stream_handle):
+    """Per-(device, stream) scratch for the split-K fix-up (zeroed once, kept zero by the kernel)."""
+    if nbytes == 0:
+        return None
+    key = (device, stream_handle)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        nbytes = max(nbytes, 1 << 20)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _lib.call("fq_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
+        _WS[key] = buf
+    return buf
+
+
+# ------------------------------------------------------------------------- weights
+
+def pack_w6(wq):
+    """int8 codes [N,K] in [-32,31] -> fq6 packed uint8 tensor."""
+    _dev(wq, torch.int8, "wq", 2)
+    N, K = wq.shape
+    _k_ok(K)
+    out = torch.empty(packed_w_bytes(N, K), dtype=torch.uint8, device=wq.device)
+    _lib.call("fq_pack_w6", _ptr(wq), N, K, _ptr(out), _stream(wq))
+    return out
+
+
+def unpack_w6(wpk, N, K):
+    _dev(wpk, torch.uint8, "w_packed", 1)
+    _k_ok(K)
+    _need(wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
+    out = torch.empty((N, K), dtype=torch.int8, device=wpk.device)
+    _lib.call("fq_unpack_w6", _ptr(wpk), N, K, _ptr(out), _stream(wpk))
+    return out
+
+
+def quantize_pack_w6(w, return_codes=False):
+    """fp16 weight [N,K] -> (fq6 packed, ws fp16 [K/128, N]) (+ int8 codes if requested)."""
+    _dev(w, torch.float16, "w", 2)
+    N, K = w.shape
+    _k_ok(K)
+    wpk = torch.empty(packed_w_bytes(N, K), dtype=torch.uint8, device=w.device)
+    ws = torch.empty((K // GROUP, N), dtype=torch.float16, device=w.device)
+    wq = torch.empty((N, K), dtype=torch.int8, device=w.device) if return_codes else None
+    _lib.call("fq_quantize_pack_w6", _ptr(w), N, K, _ptr(wpk), _ptr(ws), _ptr(wq), _stream(w))
+    return (wpk, ws, wq) if return_codes else (wpk, ws)
+
+
+# ------------------------------------------------------------------------- activations
+
+def quantize_act(x, abits):
+    """fp16 [M,K] -> (xq int8 [M,K], xs fp16 [K/128, M]) -- engine rounding semantics."""
+    _dev(x, torch.float16, "x", 2)
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    M, K = x.shape
+    _k_ok(K)
+    xq = torch.empty((M, K), dtype=torch.int8, device=x.device)
+    xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=x.device)
+    _lib.call("fq_quantize_act", _ptr(x), M, K, abits, _ptr(xq), _ptr(xs), _stream(x))
+    return xq, xs
+
+
+# ------------------------------------------------------------------------- GEMM
+
+def gemm_w6ax(xq, xs, wpk, ws, N, abits=6, return_acc=False, out=None):
+    """d fp16 [M,N] from quantized operands; with return_acc also the int32 group accumulators
+    [M, N, K/128] (bit-exact debug output)."""
+    _dev(xq, torch.int8, "xq", 2)
+    M, K = xq.shape
+    _k_ok(K)
+    _dev(xs, torch.float16, "xs", 2)
+    _need(tuple(xs.shape) == (K // GROUP, M), f"xs must be [K/128, M] = {(K // GROUP, M)}")
+    _dev(wpk, torch.uint8, "w_packed", 1)
+    _need(wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
+    _dev(ws, torch.float16, "ws", 2)
+    _need(tuple(ws.shape) == (K // GROUP, N), f"ws must be [K/128, N] = {(K // GROUP, N)}")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    dev = xq.device
+    for t in (xs, wpk, ws):
+        _need(t.device == dev, "all operands must be on one device")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=dev)
+    else:
+        _dev(out, torch.float16, "out", 2)
+        _need(tuple(out.shape) == (M, N), "out shape mismatch")
+    acc = torch.empty((M, N, K // GROUP), dtype=torch.int32, device=dev) if return_acc else None
+    s = _stream(xq)
+    nb = gemm_workspace_bytes(M, N, K)
+    wbuf = workspace(dev, nb, s.value)
+    _lib.call("fq_gemm_w6ax", _ptr(xq), _ptr(xs), _ptr(wpk), _ptr(ws), M, N, K, abits, _ptr(out),
+              _ptr(acc), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return (out, acc) if return_acc else out
+
+
+def linear_w6ax(x, wpk, ws, N, abits=6, out=None):
+    """Quantize + GEMM (FLEXQGEMMWrapper::gemm(const half* A ...)) for fp16 x [M,K]."""
+    _dev(x, torch.float16, "x", 2)
+    M, K = x.shape
+    _k_ok(K)
+    _dev(wpk, torch.uint8, "w_packed", 1)
+    _need(wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
+    _dev(ws, torch.float16, "ws", 2)
+    _need(tuple(ws.shape) == (K // GROUP, N), f"ws must be [K/128, N] = {(K // GROUP, N)}")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    dev = x.device
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=dev)
+    xq = torch.empty((M, K), dtype=torch.int8, device=dev)
+    xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=dev)
+    s = _stream(x)
+    nb = gemm_workspace_bytes(M, N, K)
+    wbuf = workspace(dev, nb, s.value)
+    _lib.call("fq_linear_w6ax", _ptr(x), M, N, K, abits, _ptr(wpk), _ptr(ws), _ptr(out), _ptr(xq),
+              _ptr(xs), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return out
+
+
+# ------------------------------------------------------------------------- reference layouts
+
+def _rows_ok(R):
+    _need(R > 0 and (R <= 8 or R % 8 == 0), f"rows={R}: the reference bit-plane layout needs <= 8 or a multiple of 8")
+
+
+def ref_bit_packing(vals, bits):
+    """flexq_bit_packing(const int*...): int32 raw b-bit patterns [R,K] -> bit planes."""
+    _dev(vals, torch.int32, "vals", 2)
+    R, K = vals.shape
+    _k_ok(K)
+    _rows_ok(R)
+    out = torch.empty(bits * R * (K // 32), dtype=torch.int32, device=vals.device)
+    _lib.call("fq_ref_bit_packing", _ptr(vals), _ptr(out), R, K, bits, _stream(vals))
+    return out
+
+
+def ref_quantize_bit_packing(x, bits):
+    """e2e flexq_bit_packing(const half*...): fp16 [M,K] -> (bit planes, x_scale_dup)."""
+    _dev(x, torch.float16, "x", 2)
+    M, K = x.shape
+    _k_ok(K)
+    _rows_ok(M)
+    _need(bits in (6, 8), "bits must be 6 or 8")
+    planes = torch.empty(bits * M * (K // 32), dtype=torch.int32, device=x.device)
+    ld = 2 * ((M + 3) // 4 * 4)
+    dup = torch.zeros((K // GROUP, ld), dtype=torch.float16, device=x.device)
+    _lib.call("fq_ref_quantize_bit_packing", _ptr(x), _ptr(planes), _ptr(dup), M, K, bits, _stream(x))
+    return planes, dup
+
+
+def import_ref_w(planes, N, K):
+    _dev(planes, torch.int32, "planes", 1)
+    _k_ok(K)
+    _rows_ok(N)
+    _need(planes.numel() == 6 * N * (K // 32), "planes size does not match 6-bit [N,K]")
+    out = torch.empty(packed_w_bytes(N, K), dtype=torch.uint8, device=planes.device)
+    _lib.call("fq_import_ref_w", _ptr(planes), N, K, _ptr(out), _stream(planes))
+    return out
+
+
+def import_ref_x(planes, dup, M, K, bits):
+    _dev(planes, torch.int32, "planes", 1)
+    _dev(dup, torch.float16, "x_scale_dup", 2)
+    _k_ok(K)
+    _rows_ok(M)
+    _need(planes.numel() == bits * M * (K // 32), "planes size does not match [M,K]")
+    xq = torch.empty((M, K), dtype=torch.int8, device=planes.device)
+    xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=planes.device)
+    _lib.call("fq_import_ref_x", _ptr(planes), _ptr(dup), M, K, bits, _ptr(xq), _ptr(xs), _stream(planes))
+    return xq, xs

@@ -1,0 +1,149 @@
+/*
+ * flexq_hip.h -- C ABI of the MI355X-native (gfx950) W6Ax quantized-linear engine.
+ *
+ * The library (flexq_amd/libflexq_hip.so) replaces the hot path of FlexQ (hoffmann-muki/FlexQ):
+ * INT6 weight packing, dynamic per-group (g = 128) INT6/INT8 activation quantization and the
+ * W6A6 / W6A8 GEMM with per-group dequantization to fp16.  Paths below are relative to the
+ * reference checkout.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Every pointer argument except where marked "host" is a
+ *     device pointer owned by the caller; the library never allocates or frees device memory
+ *     inside an entry point, never synchronises, and never prints.  All work is enqueued on the
+ *     given stream (NULL = the default stream), so every entry point is safe to capture in a HIP
+ *     graph.  fp16 values are passed as uint16_t bit patterns.
+ *   - Every entry point returns an fq_status; non-zero means nothing was enqueued (argument
+ *     errors) or the launch failed (FQ_ERR_HIP).  The reference's error behaviour was
+ *     print-and-return (flexq_gemm_wrapper.cu:44,88,93) or `initSuccess=false`
+ *     (flexq_bmma_op.h:103-126); here the same conditions return a status code instead.
+ *   - Group size is fixed at 128 along K (flexq_bmma_kernel.h:54,71); K % 128 == 0 is required
+ *     (test_bgemm_kernel.cu:173-176, flexq_gemm_wrapper.cu:43-46).  Weight bits are 6; activation
+ *     bits are 6 or 8 (the two instantiated families, flexq_bmma_library.cu:23-497).
+ *
+ * Data layouts owned by this build
+ *   xq   int8  [M][K]               activation codes (values in [-32,31] for A6, [-128,127] for A8)
+ *   xs   fp16  [K/128][M]           activation group scales
+ *   wpk  bytes fq_packed_w_bytes(N,K): "fq6" layout, 0.75 B per weight, MFMA-operand ordered
+ *   ws   fp16  [K/128][N]           weight group scales (same as the reference's W_SCALE,
+ *                                   test_bgemm_kernel.cu:57-63)
+ *   d    fp16  [M][N]               output, row-major
+ * Reference layouts (bit planes, duplicated half2 x-scales) are accepted by the fq_ref_* and
+ * fq_import_* entry points.
+ */
+#ifndef FLEXQ_HIP_H
+#define FLEXQ_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *fq_stream_t; /* == hipStream_t */
+
+typedef int fq_status;
+#define FQ_OK 0
+#define FQ_ERR_NULL 1      /* a required pointer is NULL */
+#define FQ_ERR_SHAPE 2     /* M/N/K out of the supported range (K % 128, layout limits) */
+#define FQ_ERR_BITS 3      /* unsupported bit width */
+#define FQ_ERR_WORKSPACE 4 /* workspace missing or smaller than fq_gemm_workspace_bytes() */
+#define FQ_ERR_HIP 5       /* the HIP launch itself failed */
+
+/* ---- library info ------------------------------------------------------------------------ */
+const char *fq_version(void);
+const char *fq_status_string(fq_status s);
+
+/* ---- sizes ------------------------------------------------------------------------------- */
+/* Bytes of the fq6 packed weight for an [N][K] matrix (N padded to 32 internally). */
+size_t fq_packed_w_bytes(int N, int K);
+/* Bytes of scratch fq_gemm_w6ax / fq_linear_w6ax need for this shape (0 if none).  The buffer
+ * must be zero-filled once after allocation (fq_workspace_init); the kernels leave it zeroed. */
+size_t fq_gemm_workspace_bytes(int M, int N, int K);
+fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_t stream);
+
+/* ---- weight packing (offline) ------------------------------------------------------------- */
+/* int8 weight codes [N][K] (values in [-32,31]) -> fq6.  Replaces flexq_bit_packing(const int*,
+ * int*, M, K, BIT, stream) applied to weights (engine/src/pack/bit_packing.h:34,
+ * test_bgemm_kernel.cu:222-223). */
+fq_status fq_pack_w6(const int8_t *wq, int N, int K, void *w_packed, fq_stream_t stream);
+/* Inverse, for checks: fq6 -> int8 [N][K]. */
+fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, fq_stream_t stream);
+/* fp16 weight [N][K] -> per-(row,128-group) symmetric 6-bit codes + fq6 + ws [K/128][N].
+ * Same rounding rule as fq_quantize_act (the offline converter the reference does not ship,
+ * LlamaDecoderLayerWeight.cc:381-410 loads its output). wq_out (int8 [N][K]) is optional. */
+fq_status fq_quantize_pack_w6(const uint16_t *w, int N, int K, void *w_packed, uint16_t *ws,
+                              int8_t *wq_out, fq_stream_t stream);
+
+/* ---- activation quantization (online) ----------------------------------------------------- */
+/* fp16 x [M][K] -> xq int8 [M][K], xs fp16 [K/128][M]: dynamic per-(row,128-group) symmetric
+ * quantization with the reference engine's arithmetic (e2e .../flexqgemm/src/pack/
+ * bit_packing.cu:125-164): scale = half(absmax / (2^(b-1)-1)), q = clamp(roundf(x/scale)).
+ * All-zero groups quantize to 0 (the reference's NaN path).  abits in {6, 8}. */
+fq_status fq_quantize_act(const uint16_t *x, int M, int K, int abits, int8_t *xq, uint16_t *xs,
+                          fq_stream_t stream);
+
+/* ---- GEMM ------------------------------------------------------------------------------- */
+/* d[M][N] = fp16( sum_g float(half(xs[g][m]*ws[g][n])) * acc[m][n][g] ),
+ * acc[m][n][g] = sum_{k in g} xq[m][k]*wq[n][k] (exact int32).  Replaces
+ * FQBMMAInitFn/FQBMMAExecFn (engine/src/bgemm/flexq_bmma_op.h:163-188) and
+ * FLEXQGEMMWrapper::gemm(int* A ...) (e2e .../flexq_gemm_wrapper.cu:21-97).
+ * acc_dbg: optional int32 [M][N][K/128] copy of the group accumulators (bit-exact checks).
+ * workspace: fq_gemm_workspace_bytes(M,N,K) bytes, initialised once by fq_workspace_init. */
+fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const void *w_packed,
+                       const uint16_t *ws, int M, int N, int K, int abits, uint16_t *d,
+                       int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
+                       fq_stream_t stream);
+
+/* Quantize + GEMM in one call.  Replaces FLEXQGEMMWrapper::gemm(const half* A ...)
+ * (flexq_gemm_wrapper.cu:99-122).  xq_buf/xs_buf: caller scratch of M*K bytes and
+ * 2*M*(K/128) bytes (the reference's activation workspace, LlamaV2ContextAttentionLayer.cc:793). */
+fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
+                         const uint16_t *ws, uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf,
+                         void *workspace, size_t workspace_bytes, fq_stream_t stream);
+
+/* ---- reference-layout entry points (drop-in for FlexQ's own formats) ------------------------ */
+/* flexq_bit_packing(const int* in, int* out, M, K, BIT, stream) (engine/src/pack/bit_packing.h:34,
+ * bit_packing.cu:147-156): raw b-bit patterns [M][K] -> bit planes int32
+ * [K/128][M/c][BIT][c][4], c = min(M,8), k0 at bit 31.  M must be <= 8 or a multiple of 8. */
+fq_status fq_ref_bit_packing(const int32_t *in, int32_t *packed, int M, int K, int bits,
+                             fq_stream_t stream);
+/* flexq_bit_packing(const half* in, int* out, half* x_scale, M, K, BIT, stream)
+ * (e2e .../flexqgemm/src/pack/bit_packing.h:32-34, FLEXQGEMMWrapper::pack): quantize + bit-plane
+ * pack; x_scale_dup is the reference layout half[K/128][2*ceil4(M)] of duplicated pairs. */
+fq_status fq_ref_quantize_bit_packing(const uint16_t *x, int32_t *packed, uint16_t *x_scale_dup,
+                                      int M, int K, int bits, fq_stream_t stream);
+/* Reference bit-plane weights (W_BITS = 6, [K/128][N/c][6][c][4]) -> fq6. */
+fq_status fq_import_ref_w(const int32_t *w_bitplanes, int N, int K, void *w_packed,
+                          fq_stream_t stream);
+/* Reference bit-plane activations + duplicated scales -> xq int8 [M][K] + xs [K/128][M]. */
+fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, int M, int K,
+                          int bits, int8_t *xq, uint16_t *xs, fq_stream_t stream);
+
+/* FQBMMAOpState-style two-call interface over REFERENCE-layout operands
+ * (flexq_bmma_op.h:19-34,163-188): init validates and records the arguments (no launch, no
+ * device-attribute call per init, unlike flexq_bmma_op.h:103), exec imports X from bit planes
+ * into `scratch` and runs fq_gemm_w6ax.  W must already be in fq6 (import it once with
+ * fq_import_ref_w, as FT loads pre-packed weights once).  scratch: fq_bmma_scratch_bytes(). */
+typedef struct fq_bmma_state {
+    int init_success;
+    int M, N, K, x_bits, w_bits, group_size;
+    const int32_t *X;        /* reference bit-plane activations */
+    const void *W;           /* fq6 weights */
+    const uint16_t *X_SCALE; /* reference duplicated layout */
+    const uint16_t *W_SCALE; /* [K/128][N] */
+    uint16_t *D;
+    void *scratch;
+    size_t scratch_bytes;
+} fq_bmma_state;
+size_t fq_bmma_scratch_bytes(int M, int N, int K);
+fq_bmma_state fq_bmma_init(const int32_t *X, const void *W, const uint16_t *X_SCALE,
+                           const uint16_t *W_SCALE, int M, int N, int K, uint16_t *D,
+                           int group_size, int bias, int x_bits, int w_bits, void *scratch,
+                           size_t scratch_bytes);
+fq_status fq_bmma_exec(const fq_bmma_state *state, fq_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLEXQ_HIP_H */

@@ -1,0 +1,341 @@
+/*
+ * fq_oracle.c -- CPU restatement of FlexQ's W6Ax hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the parity oracle for the HIP kernels in flexq_amd/csrc.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as the
+ * checker.  Nothing in the product path links or calls it.
+ *
+ * Every function restates one piece of the reference (paths relative to /root/reference):
+ *   fqo_pack_bitplanes     engine/src/pack/bit_packing.cu:76-133     (flexq_packing_kernel)
+ *   fqo_pack_abq           engine/src/pack/bit_packing.cu:54-72      (abq_packing_kernel, KAT twin)
+ *   fqo_unpack_bitplanes   inverse of the above, sign-extending as flexq_bmma_kernel.h:396-397
+ *   fqo_quantize_engine    e2e/src/fastertransformer/kernels/flexqgemm/src/pack/bit_packing.cu:125-164
+ *   fqo_compute_ref        engine/test_bgemm_kernel.cu:113-146        (the reference's own CPU oracle)
+ *   fqo_gemm               the contract: int32 per-group accumulators (exact) dequantised with the
+ *                          fp16-rounded scale product of flexq_bmma_kernel.h:360-364, summed in
+ *                          double and rounded once to fp16.
+ *   fqo_pack_fq6 / fqo_unpack_fq6   this build's own 6-bit weight layout --
+ *                          a model of the HIP packer, not a reference function.
+ *
+ * Parity pinning: the reference ships no kernel golden vectors (inputs are time-seeded,
+ * test_bgemm_kernel.cu:178).  The kernel-side functions are pinned by (1) the packing KAT of
+ * engine/test_packing_kernel.cu:131-148 (two independent packers must agree) and (2) agreement
+ * between fqo_gemm and the restated compute_ref within the reference's own tolerance.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+/* ---------------------------------------------------------------- fp16 helpers */
+
+static float f16_to_f32(uint16_t h) {
+    uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t exp = (h >> 10) & 0x1f;
+    uint32_t man = h & 0x3ff;
+    uint32_t bits;
+    if (exp == 0) {
+        if (man == 0) {
+            bits = sign;
+        } else { /* subnormal: renormalise */
+            int e = -1;
+            do { man <<= 1; e++; } while (!(man & 0x400));
+            man &= 0x3ff;
+            bits = sign | ((uint32_t)(127 - 15 - e) << 23) | (man << 13);
+        }
+    } else if (exp == 0x1f) {
+        bits = sign | 0x7f800000u | (man << 13);
+    } else {
+        bits = sign | ((exp + 127 - 15) << 23) | (man << 13);
+    }
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+/* round-to-nearest-even double -> fp16 (no intermediate float, so no double rounding) */
+static uint16_t f64_to_f16(double d) {
+    uint16_t sign = signbit(d) ? 0x8000 : 0;
+    double a = fabs(d);
+    if (isnan(d)) return sign | 0x7e00;
+    if (a >= 65520.0) return sign | 0x7c00; /* rounds to inf */
+    if (a < 5.9604644775390625e-08 * 0.5) return sign; /* below half the min subnormal */
+    int e;
+    (void)frexp(a, &e); /* a = m * 2^e, m in [0.5,1) */
+    /* fp16 normal range: exponent (e-1) in [-14, 15] */
+    double q;
+    if (e - 1 < -14) {
+        /* subnormal: units of 2^-24 */
+        q = a * 16777216.0; /* a / 2^-24 */
+    } else {
+        q = a * ldexp(1.0, 11 - e); /* 11 significant bits */
+    }
+    double r = nearbyint(q); /* default rounding mode = round-half-even */
+    if (e - 1 < -14) {
+        uint32_t v = (uint32_t)r; /* may become 0x400 = min normal, which is the correct encoding */
+        return sign | (uint16_t)v;
+    }
+    if (r >= 2048.0) { r /= 2.0; e += 1; }
+    int be = e - 1 + 15;
+    if (be >= 31) return sign | 0x7c00;
+    uint32_t mant = (uint32_t)r - 1024u;
+    return sign | (uint16_t)((be << 10) | mant);
+}
+
+uint16_t fqo_f32_to_f16(float f) { return f64_to_f16((double)f); }
+float fqo_f16_to_f32(uint16_t h) { return f16_to_f32(h); }
+uint16_t fqo_f64_to_f16(double d) { return f64_to_f16(d); }
+
+/* ---------------------------------------------------------------- bit-plane layout */
+
+/* bit_packing.cu:75 "[k / 128, M / chunk_M, x_bits, chunk_M, 4], chunk_M = min(chunk_M, MMA_M)";
+ * the index math is bit_packing.cu:121-127.  Rows R > 8 must be a multiple of 8: otherwise the
+ * reference's chunk offsets overlap the next K-tile (SURVEY.md §2.2 "layout hazard"). */
+static int bitplane_shape_ok(int R, int K, int bits) {
+    if (R <= 0 || K <= 0 || K % 128 != 0 || bits < 1 || bits > 8) return 0;
+    if (R > 8 && R % 8 != 0) return 0;
+    return 1;
+}
+
+static inline size_t bitplane_index(int r, int kt32, int b, int R, int bits) {
+    const int chunk = R < 8 ? R : 8;
+    const int by = kt32 / 4, kw = kt32 % 4;
+    return (size_t)by * ((size_t)R * bits * 4) + (size_t)(r / chunk) * (bits * chunk * 4) +
+           (size_t)b * (chunk * 4) + (size_t)(r % chunk) * 4 + kw;
+}
+
+/* flexq_packing_kernel: bit b of element (r, k) goes to bit (31 - k%32) of word
+ * [k/128][r/c][b][r%c][(k%128)/32] -- __brev(__ballot_sync(...)) at bit_packing.cu:109. */
+int fqo_pack_bitplanes(const int32_t *in, int R, int K, int bits, int32_t *out) {
+    if (!bitplane_shape_ok(R, K, bits)) return 1;
+    memset(out, 0, (size_t)bits * R * (K / 32) * sizeof(int32_t));
+    for (int r = 0; r < R; r++)
+        for (int kt = 0; kt < K / 32; kt++)
+            for (int b = 0; b < bits; b++) {
+                uint32_t word = 0;
+                for (int j = 0; j < 32; j++) {
+                    uint32_t bit = ((uint32_t)in[(size_t)r * K + kt * 32 + j] >> b) & 1u;
+                    word |= bit << (31 - j);
+                }
+                out[bitplane_index(r, kt, b, R, bits)] = (int32_t)word;
+            }
+    return 0;
+}
+
+/* Inverse: two's complement value, MSB plane weighted -2^(bits-1) (flexq_bmma_kernel.h:396-397,
+ * test_bgemm_kernel.cu:123-127). */
+int fqo_unpack_bitplanes(const int32_t *packed, int R, int K, int bits, int32_t *out) {
+    if (!bitplane_shape_ok(R, K, bits)) return 1;
+    for (int r = 0; r < R; r++)
+        for (int kt = 0; kt < K / 32; kt++)
+            for (int j = 0; j < 32; j++) {
+                int32_t v = 0;
+                for (int b = 0; b < bits; b++) {
+                    uint32_t word = (uint32_t)packed[bitplane_index(r, kt, b, R, bits)];
+                    int32_t bit = (word >> (31 - j)) & 1;
+                    v += (b == bits - 1) ? -(bit << b) : (bit << b);
+                }
+                out[(size_t)r * K + kt * 32 + j] = v;
+            }
+    return 0;
+}
+
+/* abq_packing_kernel (bit_packing.cu:54-72): layout [bits][R][K/32], same MSB-first order.
+ * Used only by the packing known-answer test (test_packing_kernel.cu:131-148). */
+int fqo_pack_abq(const int32_t *in, int R, int K, int bits, uint32_t *out) {
+    if (R <= 0 || K % 32 != 0) return 1;
+    const size_t L = (size_t)R * (K / 32);
+    for (int b = 0; b < bits; b++)
+        for (size_t idx = 0; idx < L; idx++) {
+            uint32_t v = 0;
+            for (int i = 0; i < 32; i++) v |= (((uint32_t)in[idx * 32 + i] >> b) & 1u) << (31 - i);
+            out[(size_t)b * L + idx] = v;
+        }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- dynamic quantizer (engine) */
+
+/* roundf(): half away from zero (CUDA round(float), e2e bit_packing.cu:160). */
+static float round_half_away(float v) {
+    float t = truncf(v);
+    if (fabsf(v - t) >= 0.5f) t += copysignf(1.0f, v);
+    return t;
+}
+
+/* Restates e2e .../flexqgemm/src/pack/bit_packing.cu:125-164 for one (row, 128-group):
+ *   maxv_h = max(-1, |x|) in fp16 (exact);  maxv = float(maxv_h) / (2^(b-1)-1)  [fp32 IEEE div]
+ *   scale_h = half(maxv) [RN];  q = clamp((int)roundf(float(x) / float(scale_h)), lo, hi)
+ * The float->int conversion is CUDA's saturating cvt.rzi: NaN -> 0, +-inf -> INT_MAX/MIN, so an
+ * all-zero group (0/0) quantises to 0 and a group whose scale underflows to 0 saturates.
+ * Outputs: q int8 [M][K] row-major; xs fp16 [K/128][M] (this build's layout, group-major). */
+int fqo_quantize_engine(const uint16_t *x, int M, int K, int bits, int8_t *q, uint16_t *xs) {
+    if (M <= 0 || K <= 0 || K % 128 != 0 || (bits != 6 && bits != 8)) return 1;
+    const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
+    for (int m = 0; m < M; m++)
+        for (int g = 0; g < K / 128; g++) {
+            const uint16_t *xg = x + (size_t)m * K + (size_t)g * 128;
+            float mx = -1.0f;
+            for (int i = 0; i < 128; i++) {
+                float a = fabsf(f16_to_f32(xg[i]));
+                if (a > mx) mx = a; /* __hmax ignores a NaN operand */
+            }
+            float maxv = mx / (float)hi;
+            uint16_t sh = fqo_f32_to_f16(maxv);
+            float r = f16_to_f32(sh);
+            xs[(size_t)g * M + m] = sh;
+            for (int i = 0; i < 128; i++) {
+                float v = round_half_away(f16_to_f32(xg[i]) / r);
+                int qi;
+                if (isnan(v)) qi = 0;
+                else if (v >= (float)hi) qi = hi;
+                else if (v <= (float)lo) qi = lo;
+                else qi = (int)v;
+                q[(size_t)m * K + (size_t)g * 128 + i] = (int8_t)qi;
+            }
+        }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- the reference's compute_ref */
+
+/* Faithful restatement of compute_ref (test_bgemm_kernel.cu:113-146) including its arithmetic:
+ * `float tmp += 1.0 * (int product) * w_scale_float * x_scale_float` -- the right-hand side is
+ * evaluated in double and added to a float accumulator, bit-pair by bit-pair, k by k.
+ * x_scale_dup is the reference layout half[K/128][2*ceil4(M)] (test_bgemm_kernel.cu:41-54). */
+int fqo_compute_ref(const int32_t *w, const uint16_t *w_scale, const int32_t *x,
+                    const uint16_t *x_scale_dup, uint16_t *ref_c, int M, int N, int K, int W_BIT,
+                    int X_BIT) {
+    if (!bitplane_shape_ok(M, K, X_BIT) || !bitplane_shape_ok(N, K, W_BIT)) return 1;
+    const int chunk_m = M < 8 ? M : 8, chunk_n = N < 8 ? N : 8;
+    const int xs_ld = 2 * ((M + 3) / 4 * 4);
+    for (int m = 0; m < M; m++)
+        for (int n = 0; n < N; n++) {
+            float tmp = 0;
+            for (int xb = 0; xb < X_BIT; xb++) {
+                int xmul = (xb == X_BIT - 1) ? -(1 << xb) : (1 << xb);
+                for (int wb = 0; wb < W_BIT; wb++) {
+                    int wmul = (wb == W_BIT - 1) ? -(1 << wb) : (1 << wb);
+                    for (int kt = 0; kt < K / 32; kt++) {
+                        int w_int = w[(kt / 4) * (N * W_BIT * 4) + (n / chunk_n) * (W_BIT * chunk_n * 4) +
+                                      wb * (chunk_n * 4) + (n % chunk_n) * 4 + (kt % 4)];
+                        int x_int = x[(kt / 4) * (M * X_BIT * 4) + (m / chunk_m) * (X_BIT * chunk_m * 4) +
+                                      xb * (chunk_m * 4) + (m % chunk_m) * 4 + (kt % 4)];
+                        float wsf = f16_to_f32(w_scale[(kt / 4) * N + n]);
+                        float xsf = f16_to_f32(x_scale_dup[(kt / 4) * xs_ld + 2 * m]);
+                        for (int k = 0; k < 32; k++) {
+                            int xv = ((1 << k) & x_int) != 0;
+                            int wv = ((1 << k) & w_int) != 0;
+                            tmp += 1.0 * (xmul * wmul * xv * wv) * wsf * xsf;
+                        }
+                    }
+                }
+            }
+            ref_c[(size_t)m * N + n] = fqo_f32_to_f16(tmp);
+        }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- the contract oracle */
+
+/* D[m][n] = half( sum_g float(half(xs[g][m] * ws[g][n])) * acc[m][n][g] ),
+ * acc[m][n][g] = sum_{k in group g} xq[m][k] * wq[n][k]  (exact int32).
+ * The scale product is rounded to fp16 exactly like __hmul2 (flexq_bmma_kernel.h:360-364): the
+ * fp32 product of two fp16 values is exact, so one RN to fp16 reproduces the hardware result.
+ * The sum over groups is done in double and rounded once (the HIP kernel sums in fp32; tests
+ * compare within 1e-3 relative plus an fp32-cancellation floor, see tests/common.py).
+ * Optional outputs: acc [M][N][K/128] int32, mag [M][N] = sum_g |s_g * acc_g| (double). */
+int fqo_gemm(const int8_t *xq, const uint16_t *xs, const int8_t *wq, const uint16_t *ws, int M, int N,
+             int K, uint16_t *out, int32_t *acc_out, double *mag_out) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 128 != 0) return 1;
+    const int G = K / 128;
+    for (int m = 0; m < M; m++)
+        for (int n = 0; n < N; n++) {
+            double sum = 0.0, mag = 0.0;
+            for (int g = 0; g < G; g++) {
+                const int8_t *xr = xq + (size_t)m * K + (size_t)g * 128;
+                const int8_t *wr = wq + (size_t)n * K + (size_t)g * 128;
+                int32_t a = 0;
+                for (int i = 0; i < 128; i++) a += (int32_t)xr[i] * (int32_t)wr[i];
+                float p = f16_to_f32(xs[(size_t)g * M + m]) * f16_to_f32(ws[(size_t)g * N + n]);
+                double s = (double)f16_to_f32(fqo_f32_to_f16(p));
+                sum += s * (double)a;
+                mag += fabs(s * (double)a);
+                if (acc_out) acc_out[((size_t)m * N + n) * G + g] = a;
+            }
+            out[(size_t)m * N + n] = f64_to_f16(sum);
+            if (mag_out) mag_out[(size_t)m * N + n] = mag;
+        }
+    return 0;
+}
+
+/* Reference x_scale layout half[K/128][2*ceil4(M)], each scale duplicated as a half2 pair and the
+ * row padding zeroed (base.h:35-39, test_bgemm_kernel.cu:41-54, e2e bit_packing.cu:152-156). */
+int fqo_xs_to_ref_dup(const uint16_t *xs, int M, int K, uint16_t *dup) {
+    const int ld = 2 * ((M + 3) / 4 * 4);
+    for (int g = 0; g < K / 128; g++)
+        for (int j = 0; j < ld; j += 2) {
+            uint16_t v = (j / 2 < M) ? xs[(size_t)g * M + j / 2] : 0;
+            dup[(size_t)g * ld + j] = v;
+            dup[(size_t)g * ld + j + 1] = v;
+        }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- this build's fq6 layout */
+
+/* Model of the HIP packer's output (flexq_amd/csrc/fq_pack.hip).  Layout:
+ *   uint32 [Npad/32][K/128][4 kstep][64 lane][3 word],  Npad = ceil(N/32)*32 (pad columns = 0).
+ *   lane l, kstep s hold column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j, j = 0..15.
+ *   byte b of word r: ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3).
+ * Unpacking (out_r = P_r & 0xFCFCFCFC, out_3 = sum_r (P_r & 0x03030303) << (2r+2)) yields 4*v as
+ * int8, i.e. the MFMA B operand scaled by 4. */
+size_t fqo_fq6_bytes(int N, int K) { return (size_t)((N + 31) / 32) * (K / 128) * 3072; }
+
+int fqo_pack_fq6(const int8_t *wq, int N, int K, uint8_t *out) {
+    if (N <= 0 || K % 128 != 0) return 1;
+    const int NT = (N + 31) / 32, G = K / 128;
+    memset(out, 0, fqo_fq6_bytes(N, K));
+    for (int t = 0; t < NT; t++)
+        for (int g = 0; g < G; g++)
+            for (int s = 0; s < 4; s++)
+                for (int l = 0; l < 64; l++) {
+                    int n = 32 * t + (l & 31);
+                    int v[16];
+                    for (int j = 0; j < 16; j++) {
+                        int k = 128 * g + 32 * s + 16 * (l >> 5) + j;
+                        v[j] = (n < N) ? wq[(size_t)n * K + k] : 0;
+                    }
+                    uint8_t *dst = out + ((((size_t)t * G + g) * 4 + s) * 64 + l) * 12;
+                    for (int r = 0; r < 3; r++)
+                        for (int b = 0; b < 4; b++)
+                            dst[4 * r + b] = (uint8_t)((((unsigned)v[4 * r + b] & 63u) << 2) |
+                                                       (((unsigned)v[12 + b] >> (2 * r)) & 3u));
+                }
+    return 0;
+}
+
+int fqo_unpack_fq6(const uint8_t *packed, int N, int K, int8_t *wq) {
+    if (N <= 0 || K % 128 != 0) return 1;
+    const int NT = (N + 31) / 32, G = K / 128;
+    for (int t = 0; t < NT; t++)
+        for (int g = 0; g < G; g++)
+            for (int s = 0; s < 4; s++)
+                for (int l = 0; l < 64; l++) {
+                    int n = 32 * t + (l & 31);
+                    if (n >= N) continue;
+                    const uint8_t *src = packed + ((((size_t)t * G + g) * 4 + s) * 64 + l) * 12;
+                    for (int j = 0; j < 16; j++) {
+                        int k = 128 * g + 32 * s + 16 * (l >> 5) + j;
+                        unsigned u;
+                        if (j < 12) {
+                            u = src[j] >> 2;
+                        } else {
+                            int b = j - 12;
+                            u = (src[b] & 3u) | ((src[4 + b] & 3u) << 2) | ((src[8 + b] & 3u) << 4);
+                        }
+                        wq[(size_t)n * K + k] = (int8_t)((int)(u << 26) >> 26);
+                    }
+                }
+    return 0;
+}

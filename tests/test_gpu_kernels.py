@@ -1,0 +1,237 @@
+"""GPU parity tests: every HIP kernel through the C ABI against the CPU oracle.
+
+Bit-exact: activation codes + scales, fq6 packing, reference bit planes, imports, the int32
+group accumulators.  fp16 outputs: within 1e-3 relative + the fp32-accumulation floor
+(oracle.gemm_tolerance).  Shapes cover the reference's edge cases: M in {1,2,4,8} (the wrapper's
+buckets, flexq_gemm_wrapper.cu:53-84) and the ragged ones the reference gets wrong (3, 5-7,
+M % 8 != 0), N not a multiple of 32, K = 128 (minimum) and K = 11008 (86 groups, odd split),
+all-zero groups, tiny/huge groups, and the A8 range.
+"""
+import numpy as np
+import pytest
+import torch
+
+from common import assert_gemm_close, kat_operands, model_operands, oracle, rng
+from inputs import act_input, edge_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from flexq_amd import ops as _ops
+    return _ops
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+# ------------------------------------------------------------------ activation quantizer
+
+@pytest.mark.parametrize("M,K", [(1, 128), (1, 4096), (3, 384), (16, 4096), (17, 11008), (64, 1024), (1000, 256)])
+@pytest.mark.parametrize("bits", [6, 8])
+def test_quantize_act_bit_exact(ops, dev, M, K, bits):
+    x = act_input(M, K, seed=M + K + bits).astype(np.float16)
+    xq, xs = ops.quantize_act(to_dev(x, dev), bits)
+    q_ref, xs_ref = oracle.quantize_engine(x, bits)
+    np.testing.assert_array_equal(host(xq), q_ref)
+    np.testing.assert_array_equal(host(xs).view(np.uint16), xs_ref.view(np.uint16))
+
+
+@pytest.mark.parametrize("bits", [6, 8])
+def test_quantize_act_edge_cases(ops, dev, bits):
+    for name, arr in edge_inputs().items():
+        x = arr.reshape(-1, arr.shape[-1]).astype(np.float16)
+        xq, xs = ops.quantize_act(to_dev(x, dev), bits)
+        q_ref, xs_ref = oracle.quantize_engine(x, bits)
+        np.testing.assert_array_equal(host(xq), q_ref, err_msg=name)
+        np.testing.assert_array_equal(host(xs).view(np.uint16), xs_ref.view(np.uint16), err_msg=name)
+    # ties at exactly .5: roundf goes away from zero (e2e bit_packing.cu:160)
+    x = np.zeros((1, 128), np.float16)
+    x[0, 0] = 31.0
+    x[0, 1:9] = [0.5, 1.5, 2.5, -0.5, -1.5, -2.5, 30.5, -31.5]
+    xq, _ = ops.quantize_act(to_dev(x, dev), 6)
+    assert list(host(xq)[0, :9]) == [31, 1, 2, 3, -1, -2, -3, 31, -32]
+
+
+# ------------------------------------------------------------------ packers and importers
+
+@pytest.mark.parametrize("N,K", [(32, 128), (64, 4096), (40, 384), (4096, 256)])
+def test_pack_w6_bit_exact(ops, dev, N, K):
+    wq = rng(N * 7 + K).integers(-32, 32, size=(N, K)).astype(np.int8)
+    pk = ops.pack_w6(to_dev(wq, dev))
+    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq))
+    np.testing.assert_array_equal(host(ops.unpack_w6(pk, N, K)), wq)
+
+
+@pytest.mark.parametrize("N,K", [(32, 128), (96, 1024), (40, 256)])
+def test_quantize_pack_w6(ops, dev, N, K):
+    w = (rng(N + K).standard_normal((N, K)) * 0.02).astype(np.float16)
+    pk, ws, wq = ops.quantize_pack_w6(to_dev(w, dev), return_codes=True)
+    wq_ref, ws_ref = oracle.quantize_engine(w, 6)
+    np.testing.assert_array_equal(host(wq), wq_ref)
+    np.testing.assert_array_equal(host(ws).view(np.uint16), ws_ref.view(np.uint16))
+    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq_ref))
+
+
+@pytest.mark.parametrize("R,K,bits", [(1, 128, 6), (4, 512, 8), (8, 256, 6), (24, 384, 6), (16, 128, 8)])
+def test_ref_bit_packing_bit_exact(ops, dev, R, K, bits):
+    vals = rng(R + K + bits).integers(0, 1 << bits, size=(R, K), dtype=np.int32)
+    planes = ops.ref_bit_packing(to_dev(vals, dev), bits)
+    np.testing.assert_array_equal(host(planes), oracle.pack_bitplanes(vals, bits))
+
+
+@pytest.mark.parametrize("M,K,bits", [(1, 4096, 6), (2, 256, 8), (4, 384, 6), (8, 1024, 8), (16, 512, 6)])
+def test_ref_quantize_bit_packing(ops, dev, M, K, bits):
+    """The drop-in for e2e flexq_bit_packing(const half*...) + FLEXQGEMMWrapper::pack."""
+    x = act_input(M, K, seed=3 * M + K).astype(np.float16)
+    planes, dup = ops.ref_quantize_bit_packing(to_dev(x, dev), bits)
+    q_ref, xs_ref = oracle.quantize_engine(x, bits)
+    np.testing.assert_array_equal(host(planes), oracle.pack_bitplanes(q_ref.astype(np.int32), bits))
+    np.testing.assert_array_equal(host(dup).view(np.uint16), oracle.xs_to_ref_dup(xs_ref, M, K).view(np.uint16))
+    xq2, xs2 = ops.import_ref_x(planes, dup, M, K, bits)
+    np.testing.assert_array_equal(host(xq2), q_ref)
+    np.testing.assert_array_equal(host(xs2).view(np.uint16), xs_ref.view(np.uint16))
+
+
+@pytest.mark.parametrize("N,K", [(8, 128), (64, 384), (48, 256)])
+def test_import_ref_w(ops, dev, N, K):
+    wraw = rng(N + K).integers(0, 64, size=(N, K), dtype=np.int32)
+    wq = ((wraw ^ 32) - 32).astype(np.int8)
+    planes = oracle.pack_bitplanes(wraw, 6)
+    pk = ops.import_ref_w(to_dev(planes, dev), N, K)
+    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq))
+
+
+# ------------------------------------------------------------------ GEMM
+
+def run_gemm(ops, dev, xq, xs, wq, ws, abits):
+    N = wq.shape[0]
+    pk = ops.pack_w6(to_dev(wq, dev))
+    args = (to_dev(xq, dev), to_dev(xs, dev), pk, to_dev(ws, dev), N, abits)
+    d, acc = ops.gemm_w6ax(*args, return_acc=True)
+    d_prod = ops.gemm_w6ax(*args)  # the production (no debug output) kernel variant
+    np.testing.assert_array_equal(host(d).view(np.uint16), host(d_prod).view(np.uint16))
+    return host(d), host(acc)
+
+
+GEMM_KAT = [
+    (1, 32, 128, 6), (1, 64, 256, 6), (2, 96, 384, 6), (3, 64, 256, 8), (4, 4096, 4096, 6),
+    (5, 40, 256, 6), (8, 64, 11008, 6), (9, 128, 512, 8), (16, 4096, 1024, 8), (17, 100, 384, 6),
+    (31, 64, 256, 6), (32, 256, 512, 8), (33, 96, 256, 6), (64, 128, 256, 6), (130, 200, 384, 8),
+    (257, 256, 1024, 6), (512, 512, 512, 8),
+]
+
+
+@pytest.mark.parametrize("M,N,K,abits", GEMM_KAT)
+def test_gemm_kat(ops, dev, M, N, K, abits):
+    """Reference-test-style operands: raw uniform bit patterns, scales U[0, 0.1)."""
+    _, _, xq, wq, xs, ws = kat_operands(M, N, K, abits, seed=M * 31 + N * 7 + K)
+    d, acc = run_gemm(ops, dev, xq, xs, wq, ws, abits)
+    ref, acc_ref, mag = oracle.gemm(xq, xs, wq, ws, want_acc=True)
+    np.testing.assert_array_equal(acc, acc_ref)  # int32 group accumulators, bit-exact
+    assert_gemm_close(d, ref, mag, f"gemm M={M} N={N} K={K} a{abits}")
+
+
+@pytest.mark.parametrize("M,N,K,abits", [(1, 4096, 4096, 6), (16, 4096, 11008, 8), (16, 11008, 4096, 6), (256, 1024, 4096, 8)])
+def test_gemm_model_like(ops, dev, M, N, K, abits):
+    _, _, xq, wq, xs, ws = model_operands(M, N, K, abits, seed=M + N + K)
+    d, acc = run_gemm(ops, dev, xq, xs, wq, ws, abits)
+    ref, acc_ref, mag = oracle.gemm(xq, xs, wq, ws, want_acc=True)
+    np.testing.assert_array_equal(acc, acc_ref)
+    assert_gemm_close(d, ref, mag, f"model-like M={M} N={N} K={K}")
+
+
+def test_gemm_zero_groups_and_extremes(ops, dev):
+    M, N, K = 4, 64, 512
+    xq = np.full((M, K), -128, np.int8)
+    xq[1, :128] = 0  # an all-zero group
+    wq = np.full((N, K), -32, np.int8)
+    wq[:, 128:256] = 31
+    xs = np.full((K // 128, M), 0.0999, np.float16)
+    ws = np.full((K // 128, N), 0.0999, np.float16)
+    d, acc = run_gemm(ops, dev, xq, xs, wq, ws, 8)
+    ref, acc_ref, mag = oracle.gemm(xq, xs, wq, ws, want_acc=True)
+    np.testing.assert_array_equal(acc, acc_ref)
+    assert acc.max() == 524288  # 128 * (-128) * (-32): the largest W6A8 group sum
+    assert_gemm_close(d, ref, mag, "extremes")
+
+
+def test_gemm_deterministic(ops, dev):
+    _, _, xq, wq, xs, ws = kat_operands(1, 4096, 4096, 6, seed=5)
+    pk = ops.pack_w6(to_dev(wq, dev))
+    a = [host(ops.gemm_w6ax(to_dev(xq, dev), to_dev(xs, dev), pk, to_dev(ws, dev), 4096, 6)) for _ in range(3)]
+    for b in a[1:]:
+        np.testing.assert_array_equal(a[0].view(np.uint16), b.view(np.uint16))
+
+
+@pytest.mark.parametrize("M,N,K,abits", [(1, 28672, 8192, 6), (8, 8192, 28672, 6), (16, 24576, 8192, 6)])
+def test_gemm_full_size_sampled_columns(ops, dev, M, N, K, abits):
+    """BASELINE sizes (LLaMA-2-70B): the whole GEMM runs on the GPU, the oracle checks a seeded
+    sample of 96 columns exactly (accumulators) and within tolerance (outputs)."""
+    r = rng(N + K)
+    xq = r.integers(-(1 << (abits - 1)), 1 << (abits - 1), size=(M, K)).astype(np.int8)
+    wq_dev = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev,
+                           generator=torch.Generator(device=dev).manual_seed(7))
+    xs = (r.random((K // 128, M)) * 0.05).astype(np.float16)
+    ws = (r.random((K // 128, N)) * 0.05).astype(np.float16)
+    pk = ops.pack_w6(wq_dev)
+    d, acc = ops.gemm_w6ax(to_dev(xq, dev), to_dev(xs, dev), pk, to_dev(ws, dev), N, abits, return_acc=True)
+    cols = np.sort(r.choice(N, size=96, replace=False))
+    cols_t = torch.from_numpy(cols).to(dev)
+    wq_s = host(wq_dev.index_select(0, cols_t))
+    ref, acc_ref, mag = oracle.gemm(xq, xs, wq_s, np.ascontiguousarray(ws[:, cols]), want_acc=True)
+    np.testing.assert_array_equal(host(acc.index_select(1, cols_t)), acc_ref)
+    assert_gemm_close(host(d)[:, cols], ref, mag, f"full-size M={M} N={N} K={K}")
+    # the packed weight round-trips at full size
+    assert torch.equal(ops.unpack_w6(pk, N, K), wq_dev)
+
+
+def test_linear_matches_quantize_then_gemm(ops, dev):
+    M, N, K = 16, 4096, 4096
+    x, w, xq, wq, xs, ws = model_operands(M, N, K, 6, seed=9)
+    pk = ops.pack_w6(to_dev(wq, dev))
+    d = host(ops.linear_w6ax(to_dev(x, dev), pk, to_dev(ws, dev), N, 6))
+    ref, _, mag = oracle.gemm(xq, xs, wq, ws)
+    assert_gemm_close(d, ref, mag, "linear")
+
+
+def test_bmma_state_api_reference_layout(ops, dev):
+    """FQBMMAInitFn/ExecFn-style call on reference bit-plane X (flexq_bmma_op.h:163-188)."""
+    import ctypes
+    from flexq_amd import _lib
+    M, N, K, abits = 4, 256, 1024, 6
+    xraw, wraw, xq, wq, xs, ws = kat_operands(M, N, K, abits, seed=77)
+    X = to_dev(oracle.pack_bitplanes(xraw, abits), dev)
+    W = ops.import_ref_w(to_dev(oracle.pack_bitplanes(wraw, 6), dev), N, K)
+    XS = to_dev(oracle.xs_to_ref_dup(xs, M, K), dev)
+    WS = to_dev(ws, dev)
+    D = torch.empty((M, N), dtype=torch.float16, device=dev)
+    L = _lib.load()
+    nb = L.fq_bmma_scratch_bytes(M, N, K)
+    scratch = torch.zeros(max(nb, 1), dtype=torch.uint8, device=dev)
+
+    class State(ctypes.Structure):
+        _fields_ = [("init_success", ctypes.c_int), ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+                    ("x_bits", ctypes.c_int), ("w_bits", ctypes.c_int), ("group_size", ctypes.c_int),
+                    ("X", ctypes.c_void_p), ("W", ctypes.c_void_p), ("X_SCALE", ctypes.c_void_p),
+                    ("W_SCALE", ctypes.c_void_p), ("D", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
+                    ("scratch_bytes", ctypes.c_size_t)]
+    L.fq_bmma_init.restype = State
+    L.fq_bmma_init.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_size_t]
+    L.fq_bmma_exec.argtypes = [ctypes.POINTER(State), ctypes.c_void_p]
+    st = L.fq_bmma_init(X.data_ptr(), W.data_ptr(), XS.data_ptr(), WS.data_ptr(), M, N, K, D.data_ptr(), 128, 0,
+                        abits, 6, scratch.data_ptr(), scratch.numel())
+    assert st.init_success == 1
+    bad = L.fq_bmma_init(X.data_ptr(), W.data_ptr(), XS.data_ptr(), WS.data_ptr(), M, N, K, D.data_ptr(), 64, 0,
+                         abits, 6, scratch.data_ptr(), scratch.numel())
+    assert bad.init_success == 0  # group_size != 128 is rejected like FQBMMAOp::initialize
+    assert L.fq_bmma_exec(ctypes.byref(st), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    ref, _, mag = oracle.gemm(xq, xs, wq, ws)
+    assert_gemm_close(host(D), ref, mag, "bmma state api")
