@@ -1,0 +1,280 @@
+"""bench.py -- W6A6 linear-stack throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): LLaMA-2-7B, every linear layer of all 32 decoder layers,
+W6A6 group 128, batch 1 (M = 1), random-init weights of that architecture, synthetic fp16
+activations resident in HBM.  One "step" = one token through the 32-layer linear stack:
+per layer 4 dynamic activation quantizations + 5 GEMMs (qkv 12288x4096, o 4096x4096,
+gate/up 11008x4096 sharing one quantized input, down 4096x11008), captured into one HIP graph.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): column-parallel N-shard of every linear, each
+rank packs and streams only its N/P rows, then ONE all-gather per linear of the dequantized
+fp16 output over xGMI.  Total work is fixed, so "scaling" is "strong".
+
+Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
+GEMM) and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
+forward, timed on a bounded sample on this host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from flexq_amd import ops  # noqa: E402
+
+GROUP = 128
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF dense bf16)
+
+CONFIGS = {
+    # name: (layers, M, [(linear, N, K, abits)], description)
+    "llama2-7b-m1": (32, 1, [("qkv", 12288, 4096, 6), ("o", 4096, 4096, 6), ("gate", 11008, 4096, 6),
+                             ("up", 11008, 4096, 6), ("down", 4096, 11008, 6)],
+                     "LLaMA-2-7B all linear shapes, W6A6 g128, batch 1"),
+    "llama2-7b-m16": (32, 16, [("qkv", 12288, 4096, 6), ("o", 4096, 4096, 6), ("gate", 11008, 4096, 6),
+                               ("up", 11008, 4096, 6), ("down", 4096, 11008, 8)],
+                      "LLaMA-2-7B, W6A6 + W6A8 down_proj, batch 16"),
+    "llama2-70b-m1": (80, 1, [("qkv", 10240, 8192, 6), ("o", 8192, 8192, 6), ("gate", 28672, 8192, 6),
+                              ("up", 28672, 8192, 6), ("down", 8192, 28672, 6)],
+                      "LLaMA-2-70B all linear shapes (GQA qkv), W6A6 g128, batch 1"),
+}
+
+
+def alg_bytes(M, N, K, abits):
+    """Algorithmic HBM bytes of one GEMM launch: packed W (0.75 B/w) + W scales
+    + int8 X + X scales + fp16 D."""
+    return N * K * 6 // 8 + 2 * N * K // GROUP + M * K + 2 * M * K // GROUP + 2 * M * N
+
+
+def build_stack(cfg, rank, world, dev, seed=1234):
+    layers, M, lins, _ = cfg
+    g = torch.Generator(device=dev).manual_seed(seed + rank)
+    stack = []
+    for _ in range(layers):
+        L = {}
+        for (name, N, K, abits) in lins:
+            assert N % (32 * world) == 0, f"{name}: N={N} not divisible into 32-column shards for {world} ranks"
+            Nl = N // world
+            wq = torch.randint(-32, 32, (Nl, K), dtype=torch.int8, device=dev, generator=g)
+            pk = ops.pack_w6(wq)
+            del wq
+            ws = (torch.rand((K // GROUP, Nl), device=dev, generator=g) * 0.02 + 1e-3).half()
+            out = torch.empty((M, Nl), dtype=torch.float16, device=dev)
+            full = torch.empty((world * M * Nl,), dtype=torch.float16, device=dev) if world > 1 else None
+            L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, ws=ws, out=out, full=full)
+        # synthetic fp16 inputs of each linear (attention / activation outputs are out of scope)
+        for name in ("qkv", "o", "gate", "down"):
+            K = L[name]["K"]
+            L[name]["x"] = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+        stack.append(L)
+    return stack
+
+
+def run_step(stack, M, world, group=None, gemm_only=False, pre=None):
+    """One token through the linear stack.  pre: pre-quantized inputs for gemm_only."""
+    for li, L in enumerate(stack):
+        for name in ("qkv", "o", "gate", "up", "down"):
+            p = L[name]
+            src = "gate" if name == "up" else name
+            if gemm_only:
+                xq, xs = pre[li][src]
+            elif name != "up":
+                xq, xs = ops.quantize_act(L[src]["x"], p["abits"])
+                L["_q"] = (xq, xs)
+            else:
+                xq, xs = L["_q"]
+            ops.gemm_w6ax(xq, xs, p["pk"], p["ws"], p["Nl"], p["abits"], out=p["out"])
+            if world > 1 and not gemm_only:
+                dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
+
+
+def prequantize(stack):
+    pre = []
+    for L in stack:
+        d = {}
+        for name in ("qkv", "o", "gate", "down"):
+            d[name] = ops.quantize_act(L[name]["x"], L[name]["abits"])
+        pre.append(d)
+    return pre
+
+
+def capture(fn, stream):
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        fn()
+    return g
+
+
+def time_graph(g, reps, stream):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        s.record(stream)
+        for _ in range(reps):
+            g.replay()
+        e.record(stream)
+    e.synchronize()
+    return s.elapsed_time(e) / 1e3  # seconds
+
+
+def cpu_baseline(budget_s=15.0):
+    """The reference's CPU fake-quant QuantLinear forward (oracle restatement, torch CPU ops) on a
+    bounded sample: LLaMA-2-7B linear shapes at M=1, fp16, weights re-fake-quantised every forward
+    as the reference eval flow does (flexqllm.py:106-108 + int_linear.py:60-61)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import fq_oracle as oracle  # bench's cpu_baseline leg only
+    # the GPU box exports OMP_NUM_THREADS = its CPU share (os.cpu_count() reports the whole host)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    shapes = [(12288, 4096), (4096, 4096), (11008, 4096), (11008, 4096), (4096, 11008)]
+    gen = torch.Generator().manual_seed(0)
+    ws = [torch.randn((N, K), generator=gen).mul_(0.02).half() for (N, K) in shapes]
+    xs = [torch.randn((1, K), generator=gen).half() for (N, K) in shapes]
+    flops = 0.0
+    layers = 0
+    t0 = time.perf_counter()
+    while True:
+        for (N, K), w, x in zip(shapes, ws, xs):
+            oracle.quant_linear_forward(x, w, 6, 6, requant_weight=True)
+            flops += 2.0 * N * K
+        layers += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=flops / dt / 1e12, unit="TFLOPS-equiv", cores=threads, kind="port",
+                sample=f"{layers} LLaMA-2-7B layers' 5 linears (M=1, fp16) through the fake-quant "
+                       f"QuantLinear forward with per-forward weight requantisation, {dt:.1f} s, "
+                       f"{1.0 * layers / dt / 32:.4f} tok/s-equivalent",
+                tok_per_s=layers / dt / 32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="llama2-7b-m1", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline (0 = skip)")
+    ap.add_argument("--roofline-reps", type=int, default=10)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = CONFIGS[a.config]
+    layers, M, lins, desc = cfg
+    stack = build_stack(cfg, rank, world, dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+
+    # warm the per-stream workspace and RCCL communicators eagerly, on the capture stream
+    with torch.cuda.stream(stream):
+        run_step(stack, M, world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+    if a.no_graph:
+        def replay():
+            with torch.cuda.stream(stream):
+                run_step(stack, M, world)
+    else:
+        graph = capture(lambda: run_step(stack, M, world), stream)
+
+        def replay():
+            graph.replay()
+
+    with torch.cuda.stream(stream):
+        for _ in range(a.warmup):
+            replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for _ in range(a.steps):
+            replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
+    value = flops_step * a.steps / elapsed / 1e12
+    tok_s = M * a.steps / elapsed
+
+    # roofline of the dominant kernel (the decode GEMM): a graph of the step's GEMM launches only
+    pre = prequantize(stack)
+    torch.cuda.synchronize()
+    g2 = capture(lambda: run_step(stack, M, world, gemm_only=True, pre=pre), stream)
+    for _ in range(2):
+        g2.replay()
+    torch.cuda.synchronize()
+    t_g = time_graph(g2, a.roofline_reps, stream)
+    launches = layers * len(lins)
+    per_launch_s = t_g / (a.roofline_reps * launches)
+    bytes_launch = layers * sum(alg_bytes(M, N // world, K, ab) for (_, N, K, ab) in lins) / launches
+    achieved = bytes_launch / per_launch_s / 1e9
+
+    res = {
+        "metric": "W6A6 GEMM TFLOPS-equiv + tok/s on LLaMA-2-7B linear shapes, 1/2/4/8 GPU",
+        "value": round(value, 4),
+        "unit": "TFLOPS-equiv",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int8-mfma(w6a6)->fp16",
+        "data": "synthetic (random-init int6 weights of the architecture, N(0,1) fp16 activations)",
+        "tok_per_s": round(tok_s, 2),
+        "config": {
+            "workload": desc + ", linear stack of every decoder layer per step (HIP graph)",
+            "layers": layers, "batch_M": M,
+            "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
+            "parallelism": f"tp{world} column-parallel + RCCL all-gather per linear" if world > 1 else "single GPU",
+            "graph": not a.no_graph,
+        },
+        "roofline": {
+            "kernel": "fq_gemm_decode_kernel",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "per_launch_us": round(per_launch_s * 1e6, 3),
+            "alg_bytes_per_launch": int(bytes_launch),
+            "method": "graph of the step's GEMM launches only, HIP events on the capture stream",
+        },
+    }
+    if rank == 0 and world == 1 and a.cpu_budget > 0:
+        res["cpu_baseline"] = cpu_baseline(a.cpu_budget)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -161,88 +161,99 @@ extern "C" fq_status fq_ref_bit_packing(const int32_t *in, int32_t *packed, int 
 
 // =============================================================================================
 // fq6 weight layout (oracle fqo_pack_fq6):
-//   uint32 [Npad/32][K/128][4 kstep][64 lane][3 word]
+//   uint32 [Npad/32][K/128][3 plane r][64 lane][4 kstep s]
 //   lane l, kstep s: column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j (j = 0..15)
-//   byte b of word r = ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3)
-// One thread builds one lane's 12 bytes, so a wave writes one 768-byte contiguous run.
+//   byte b of word (r, s) = ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3)
+// One thread builds one lane's 48 bytes of a (tile, group) block and writes its three 16-byte
+// plane words, so each wave writes three 1 KiB contiguous runs.
 // =============================================================================================
-__device__ __forceinline__ void fq6_encode(const int v[16], uint32_t out[3]) {
+__device__ __forceinline__ uint32_t fq6_word(const int v[16], int r) {
+    uint32_t w = 0;
 #pragma unroll
-    for (int r = 0; r < 3; r++) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            uint32_t byte = (((uint32_t)v[4 * r + b] & 63u) << 2) | (((uint32_t)v[12 + b] >> (2 * r)) & 3u);
-            w |= byte << (8 * b);
-        }
-        out[r] = w;
+    for (int b = 0; b < 4; b++) {
+        uint32_t byte = (((uint32_t)v[4 * r + b] & 63u) << 2) | (((uint32_t)v[12 + b] >> (2 * r)) & 3u);
+        w |= byte << (8 * b);
     }
+    return w;
 }
 
-__device__ __forceinline__ void fq6_slot(long slot, int G, int &n, int &k0) {
-    // slot = ((t*G + g)*4 + s)*64 + l
-    const int l = (int)(slot & 63);
-    const long tgs = slot >> 6;
-    const int s = (int)(tgs & 3);
-    const long tg = tgs >> 2;
-    const int g = (int)(tg % G);
-    const int t = (int)(tg / G);
-    n = 32 * t + (l & 31);
-    k0 = 128 * g + 32 * s + 16 * (l >> 5);
+// slot = (t*G + g)*64 + l
+__device__ __forceinline__ void fq6_lane(long slot, int G, int &t, int &g, int &l) {
+    l = (int)(slot & 63);
+    const long tg = slot >> 6;
+    g = (int)(tg % G);
+    t = (int)(tg / G);
+}
+
+__device__ __forceinline__ void fq6_store(uint32_t *__restrict__ out, long slot, int l, const uint32_t p[3][4]) {
+    const long base = (slot >> 6) * 768 + l * 4;  // ((t*G+g)*3 + r)*256 + l*4
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+        *reinterpret_cast<uint4 *>(out + base + r * 256) = make_uint4(p[r][0], p[r][1], p[r][2], p[r][3]);
 }
 
 __global__ void fq_pack_w6_kernel(const int8_t *__restrict__ wq, int N, int K,
                                   uint32_t *__restrict__ out) {
     const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 4 * 64;
+    const long total = (long)NT * G * 64;
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
-        int n, k0;
-        fq6_slot(slot, G, n, k0);
-        int v[16];
-        if (n < N) {
-            const int4 raw = *reinterpret_cast<const int4 *>(wq + (long)n * K + k0);
-            const int w[4] = {raw.x, raw.y, raw.z, raw.w};
+        int t, g, l;
+        fq6_lane(slot, G, t, g, l);
+        const int n = 32 * t + (l & 31);
+        uint32_t p[3][4];
 #pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = (int)(int8_t)((w[j >> 2] >> (8 * (j & 3))) & 255);
-        } else {
+        for (int s = 0; s < 4; s++) {
+            int v[16];
+            if (n < N) {
+                const int4 raw = *reinterpret_cast<const int4 *>(wq + (long)n * K + 128 * g + 32 * s + 16 * (l >> 5));
+                const int w[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = 0;
+                for (int j = 0; j < 16; j++) v[j] = (int)(int8_t)((w[j >> 2] >> (8 * (j & 3))) & 255);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; j++) v[j] = 0;
+            }
+#pragma unroll
+            for (int r = 0; r < 3; r++) p[r][s] = fq6_word(v, r);
         }
-        uint32_t p[3];
-        fq6_encode(v, p);
-        uint32_t *dst = out + slot * 3;
-        dst[0] = p[0];
-        dst[1] = p[1];
-        dst[2] = p[2];
+        fq6_store(out, slot, l, p);
     }
 }
 
 __global__ void fq_unpack_w6_kernel(const uint32_t *__restrict__ in, int N, int K,
                                     int8_t *__restrict__ wq) {
     const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 4 * 64;
+    const long total = (long)NT * G * 64;
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
-        int n, k0;
-        fq6_slot(slot, G, n, k0);
+        int t, g, l;
+        fq6_lane(slot, G, t, g, l);
+        const int n = 32 * t + (l & 31);
         if (n >= N) continue;
-        const uint32_t *src = in + slot * 3;
-        v4i o = unpack_fq6(src[0], src[1], src[2]);
-        int4 res;
-        int *rp = reinterpret_cast<int *>(&res);
+        const long base = (slot >> 6) * 768 + l * 4;
+        const uint4 P0 = *reinterpret_cast<const uint4 *>(in + base);
+        const uint4 P1 = *reinterpret_cast<const uint4 *>(in + base + 256);
+        const uint4 P2 = *reinterpret_cast<const uint4 *>(in + base + 512);
+        const uint32_t q0[4] = {P0.x, P0.y, P0.z, P0.w}, q1[4] = {P1.x, P1.y, P1.z, P1.w},
+                       q2[4] = {P2.x, P2.y, P2.z, P2.w};
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-            // each byte holds 4*w; arithmetic shift per byte
-            uint32_t x = (uint32_t)o[d], y = 0;
+        for (int s = 0; s < 4; s++) {
+            v4i o = unpack_fq6(q0[s], q1[s], q2[s]);
+            int4 res;
+            int *rp = reinterpret_cast<int *>(&res);
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                int8_t w = (int8_t)(x >> (8 * b)) >> 2;
-                y |= ((uint32_t)(uint8_t)w) << (8 * b);
+            for (int d = 0; d < 4; d++) {
+                uint32_t x = (uint32_t)o[d], y = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    int8_t w = (int8_t)(x >> (8 * b)) >> 2;  // each byte holds 4*w
+                    y |= ((uint32_t)(uint8_t)w) << (8 * b);
+                }
+                rp[d] = (int)y;
             }
-            rp[d] = (int)y;
+            *reinterpret_cast<int4 *>(wq + (long)n * K + 128 * g + 32 * s + 16 * (l >> 5)) = res;
         }
-        *reinterpret_cast<int4 *>(wq + (long)n * K + k0) = res;
     }
 }
 
@@ -260,7 +271,7 @@ extern "C" size_t fq_packed_w_bytes(int N, int K) {
 extern "C" fq_status fq_pack_w6(const int8_t *wq, int N, int K, void *w_packed, fq_stream_t stream) {
     if (!wq || !w_packed) return FQ_ERR_NULL;
     if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
     hipLaunchKernelGGL(fq_pack_w6_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                        wq, N, K, (uint32_t *)w_packed);
     FQ_LAUNCH_CHECK();
@@ -270,7 +281,7 @@ extern "C" fq_status fq_pack_w6(const int8_t *wq, int N, int K, void *w_packed, 
 extern "C" fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, fq_stream_t stream) {
     if (!wq || !w_packed) return FQ_ERR_NULL;
     if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
     hipLaunchKernelGGL(fq_unpack_w6_kernel, dim3(grid_for(total)), dim3(256), 0,
                        (hipStream_t)stream, (const uint32_t *)w_packed, N, K, wq);
     FQ_LAUNCH_CHECK();
@@ -308,38 +319,41 @@ __global__ void fq_weight_pack_kernel(const uint16_t *__restrict__ w, const uint
                                       int N, int K, uint32_t *__restrict__ out,
                                       int8_t *__restrict__ wq_out) {
     const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 4 * 64;
+    const long total = (long)NT * G * 64;
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
-        int n, k0;
-        fq6_slot(slot, G, n, k0);
-        int v[16];
-        if (n < N) {
-            const float r = h2f(ws[(long)(k0 / FQ_GROUP) * N + n]);
-            const uint4 *src = reinterpret_cast<const uint4 *>(w + (long)n * K + k0);
-            const uint4 a = src[0], b = src[1];
-            const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        int t, g, l;
+        fq6_lane(slot, G, t, g, l);
+        const int n = 32 * t + (l & 31);
+        uint32_t p[3][4];
+        const float r = (n < N) ? h2f(ws[(long)g * N + n]) : 1.0f;
 #pragma unroll
-            for (int j = 0; j < 16; j++)
-                v[j] = sat_clamp(round_half_away(h2f((uint16_t)(d[j >> 1] >> (16 * (j & 1)))) / r), -32, 31);
-            if (wq_out) {
-                uint32_t pk[4];
+        for (int s = 0; s < 4; s++) {
+            const int k0 = 128 * g + 32 * s + 16 * (l >> 5);
+            int v[16];
+            if (n < N) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(w + (long)n * K + k0);
+                const uint4 a = src[0], b = src[1];
+                const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    pk[q] = (v[4 * q] & 255) | ((v[4 * q + 1] & 255) << 8) | ((v[4 * q + 2] & 255) << 16) |
-                            ((uint32_t)(v[4 * q + 3] & 255) << 24);
-                *reinterpret_cast<uint4 *>(wq_out + (long)n * K + k0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                for (int j = 0; j < 16; j++)
+                    v[j] = sat_clamp(round_half_away(h2f((uint16_t)(d[j >> 1] >> (16 * (j & 1)))) / r), -32, 31);
+                if (wq_out) {
+                    uint32_t pk[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        pk[q] = (v[4 * q] & 255) | ((v[4 * q + 1] & 255) << 8) | ((v[4 * q + 2] & 255) << 16) |
+                                ((uint32_t)(v[4 * q + 3] & 255) << 24);
+                    *reinterpret_cast<uint4 *>(wq_out + (long)n * K + k0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; j++) v[j] = 0;
             }
-        } else {
 #pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = 0;
+            for (int rr = 0; rr < 3; rr++) p[rr][s] = fq6_word(v, rr);
         }
-        uint32_t p[3];
-        fq6_encode(v, p);
-        uint32_t *dst = out + slot * 3;
-        dst[0] = p[0];
-        dst[1] = p[1];
-        dst[2] = p[2];
+        fq6_store(out, slot, l, p);
     }
 }
 
@@ -350,7 +364,7 @@ extern "C" fq_status fq_quantize_pack_w6(const uint16_t *w, int N, int K, void *
     hipLaunchKernelGGL(fq_weight_scale_kernel, dim3(quant_grid((long)N * (K / FQ_GROUP))), dim3(256),
                        0, (hipStream_t)stream, w, N, K, ws);
     FQ_LAUNCH_CHECK();
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
     hipLaunchKernelGGL(fq_weight_pack_kernel, dim3(grid_for(total)), dim3(256), 0,
                        (hipStream_t)stream, w, ws, N, K, (uint32_t *)w_packed, wq_out);
     FQ_LAUNCH_CHECK();
@@ -375,20 +389,23 @@ __device__ __forceinline__ int bitplane_value(const int32_t *__restrict__ planes
 __global__ void fq_import_ref_w_kernel(const int32_t *__restrict__ planes, int N, int K,
                                        uint32_t *__restrict__ out) {
     const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 4 * 64;
+    const long total = (long)NT * G * 64;
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
-        int n, k0;
-        fq6_slot(slot, G, n, k0);
-        int v[16];
+        int t, g, l;
+        fq6_lane(slot, G, t, g, l);
+        const int n = 32 * t + (l & 31);
+        uint32_t p[3][4];
 #pragma unroll
-        for (int j = 0; j < 16; j++) v[j] = (n < N) ? bitplane_value(planes, N, 6, n, k0 + j) : 0;
-        uint32_t p[3];
-        fq6_encode(v, p);
-        uint32_t *dst = out + slot * 3;
-        dst[0] = p[0];
-        dst[1] = p[1];
-        dst[2] = p[2];
+        for (int s = 0; s < 4; s++) {
+            int v[16];
+            const int k0 = 128 * g + 32 * s + 16 * (l >> 5);
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = (n < N) ? bitplane_value(planes, N, 6, n, k0 + j) : 0;
+#pragma unroll
+            for (int r = 0; r < 3; r++) p[r][s] = fq6_word(v, r);
+        }
+        fq6_store(out, slot, l, p);
     }
 }
 
@@ -409,7 +426,7 @@ extern "C" fq_status fq_import_ref_w(const int32_t *w_bitplanes, int N, int K, v
                                      fq_stream_t stream) {
     if (!w_bitplanes || !w_packed) return FQ_ERR_NULL;
     if (N <= 0 || K <= 0 || K % FQ_GROUP || (N > 8 && N % 8)) return FQ_ERR_SHAPE;
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 256;
+    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
     hipLaunchKernelGGL(fq_import_ref_w_kernel, dim3(grid_for(total)), dim3(256), 0,
                        (hipStream_t)stream, w_bitplanes, N, K, (uint32_t *)w_packed);
     FQ_LAUNCH_CHECK();

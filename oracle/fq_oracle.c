@@ -284,17 +284,24 @@ int fqo_xs_to_ref_dup(const uint16_t *xs, int M, int K, uint16_t *dup) {
 
 /* ---------------------------------------------------------------- this build's fq6 layout */
 
-/* Model of the HIP packer's output (flexq_amd/csrc/fq_pack.hip).  Layout:
- *   uint32 [Npad/32][K/128][4 kstep][64 lane][3 word],  Npad = ceil(N/32)*32 (pad columns = 0).
- *   lane l, kstep s hold column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j, j = 0..15.
- *   byte b of word r: ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3).
- * Unpacking (out_r = P_r & 0xFCFCFCFC, out_3 = sum_r (P_r & 0x03030303) << (2r+2)) yields 4*v as
- * int8, i.e. the MFMA B operand scaled by 4. */
+/* Model of the HIP packer's output (flexq_amd/csrc/fq_quant.hip).  Layout:
+ *   uint32 [Npad/32][K/128][3 plane r][64 lane][4 kstep s],  Npad = ceil(N/32)*32 (pad cols = 0)
+ *   lane l, kstep s hold column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j, j = 0..15;
+ *   byte b of word (r, s): ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3).
+ * A (tile, group) block is 3 KiB = three 1 KiB planes; lane l's plane r is 16 contiguous bytes,
+ * so one dwordx4 / LDS-DMA wave instruction moves one plane.  Unpacking (out_r = P_r &
+ * 0xFCFCFCFC, out_3 = sum_r (P_r & 0x03030303) << (2r+2)) yields 4*v as int8: the MFMA B
+ * operand scaled by 4. */
 size_t fqo_fq6_bytes(int N, int K) { return (size_t)((N + 31) / 32) * (K / 128) * 3072; }
+
+static inline size_t fq6_word(int t, int g, int r, int l, int s, int G) {
+    return ((((size_t)t * G + g) * 3 + r) * 64 + l) * 4 + s;
+}
 
 int fqo_pack_fq6(const int8_t *wq, int N, int K, uint8_t *out) {
     if (N <= 0 || K % 128 != 0) return 1;
     const int NT = (N + 31) / 32, G = K / 128;
+    uint32_t *o = (uint32_t *)out;
     memset(out, 0, fqo_fq6_bytes(N, K));
     for (int t = 0; t < NT; t++)
         for (int g = 0; g < G; g++)
@@ -306,11 +313,13 @@ int fqo_pack_fq6(const int8_t *wq, int N, int K, uint8_t *out) {
                         int k = 128 * g + 32 * s + 16 * (l >> 5) + j;
                         v[j] = (n < N) ? wq[(size_t)n * K + k] : 0;
                     }
-                    uint8_t *dst = out + ((((size_t)t * G + g) * 4 + s) * 64 + l) * 12;
-                    for (int r = 0; r < 3; r++)
+                    for (int r = 0; r < 3; r++) {
+                        uint32_t w = 0;
                         for (int b = 0; b < 4; b++)
-                            dst[4 * r + b] = (uint8_t)((((unsigned)v[4 * r + b] & 63u) << 2) |
-                                                       (((unsigned)v[12 + b] >> (2 * r)) & 3u));
+                            w |= (uint32_t)((((unsigned)v[4 * r + b] & 63u) << 2) |
+                                            (((unsigned)v[12 + b] >> (2 * r)) & 3u)) << (8 * b);
+                        o[fq6_word(t, g, r, l, s, G)] = w;
+                    }
                 }
     return 0;
 }
@@ -318,21 +327,24 @@ int fqo_pack_fq6(const int8_t *wq, int N, int K, uint8_t *out) {
 int fqo_unpack_fq6(const uint8_t *packed, int N, int K, int8_t *wq) {
     if (N <= 0 || K % 128 != 0) return 1;
     const int NT = (N + 31) / 32, G = K / 128;
+    const uint32_t *p = (const uint32_t *)packed;
     for (int t = 0; t < NT; t++)
         for (int g = 0; g < G; g++)
             for (int s = 0; s < 4; s++)
                 for (int l = 0; l < 64; l++) {
                     int n = 32 * t + (l & 31);
                     if (n >= N) continue;
-                    const uint8_t *src = packed + ((((size_t)t * G + g) * 4 + s) * 64 + l) * 12;
+                    uint32_t w[3];
+                    for (int r = 0; r < 3; r++) w[r] = p[fq6_word(t, g, r, l, s, G)];
                     for (int j = 0; j < 16; j++) {
                         int k = 128 * g + 32 * s + 16 * (l >> 5) + j;
                         unsigned u;
                         if (j < 12) {
-                            u = src[j] >> 2;
+                            u = ((w[j / 4] >> (8 * (j % 4))) & 0xffu) >> 2;
                         } else {
                             int b = j - 12;
-                            u = (src[b] & 3u) | ((src[4 + b] & 3u) << 2) | ((src[8 + b] & 3u) << 4);
+                            u = 0;
+                            for (int r = 0; r < 3; r++) u |= ((w[r] >> (8 * b)) & 3u) << (2 * r);
                         }
                         wq[(size_t)n * K + k] = (int8_t)((int)(u << 26) >> 26);
                     }

@@ -55,9 +55,10 @@ def test_quantize_act_edge_cases(ops, dev, bits):
     # ties at exactly .5: roundf goes away from zero (e2e bit_packing.cu:160)
     x = np.zeros((1, 128), np.float16)
     x[0, 0] = 31.0
-    x[0, 1:9] = [0.5, 1.5, 2.5, -0.5, -1.5, -2.5, 30.5, -31.5]
+    x[0, 1:9] = [0.5, 1.5, 2.5, -0.5, -1.5, -2.5, 30.5, -30.5]  # absmax 31 -> scale exactly 1
     xq, _ = ops.quantize_act(to_dev(x, dev), 6)
-    assert list(host(xq)[0, :9]) == [31, 1, 2, 3, -1, -2, -3, 31, -32]
+    assert list(host(xq)[0, :9]) == [31, 1, 2, 3, -1, -2, -3, 31, -31]
+    np.testing.assert_array_equal(host(xq), oracle.quantize_engine(x, 6)[0])
 
 
 # ------------------------------------------------------------------ packers and importers

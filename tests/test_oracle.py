@@ -113,12 +113,12 @@ def test_fq6_roundtrip(N, K):
 
 def test_fq6_unpack_rule_gives_4w():
     """The documented register unpack (out_r = P_r & 0xFC.., out_3 from the low bit pairs) yields
-    4*w per byte for every lane of one (tile, group) block."""
+    4*w per byte for every lane and k-step of one (tile, group) block [3 planes][64 lanes][4 steps]."""
     wq = rng(3).integers(-32, 32, size=(32, 128)).astype(np.int8)
-    pk = oracle.pack_fq6(wq).view(np.uint32).reshape(4, 64, 3)
+    pk = oracle.pack_fq6(wq).view(np.uint32).reshape(3, 64, 4)
     for s in range(4):
         for lane in range(64):
-            p0, p1, p2 = (int(v) for v in pk[s, lane])
+            p0, p1, p2 = (int(pk[r, lane, s]) for r in range(3))
             o = [p0 & 0xFCFCFCFC, p1 & 0xFCFCFCFC, p2 & 0xFCFCFCFC,
                  ((p0 & 0x03030303) << 2) | ((p1 & 0x03030303) << 4) | ((p2 & 0x03030303) << 6)]
             bts = np.frombuffer(np.array(o, dtype=np.uint32).tobytes(), dtype=np.int8)
