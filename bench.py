@@ -2,16 +2,17 @@
 
 Workload (BASELINE.json configs[1]): LLaMA-2-7B, every linear layer of all 32 decoder layers,
 W6A6 group 128, batch 1 (M = 1), random-init weights of that architecture, synthetic fp16
-activations resident in HBM.  One "step" = one token through the 32-layer linear stack:
-per layer 4 dynamic activation quantizations + 5 GEMMs (qkv 12288x4096, o 4096x4096,
-gate/up 11008x4096 sharing one quantized input, down 4096x11008), captured into one HIP graph.
+activations resident in HBM.  One "step" = one token through the 32-layer linear stack: per
+layer 5 W6A6 linears (qkv 12288x4096, o 4096x4096, gate/up 11008x4096 reading the same input,
+down 4096x11008), each one fq_linear_w6ax call = dynamic activation quantization + GEMM +
+dequant (at decode sizes a single fused launch), captured into one HIP graph.
 
 Multi-GPU (torchrun, one process per GPU, RCCL): column-parallel N-shard of every linear, each
 rank packs and streams only its N/P rows, then ONE all-gather per linear of the dequantized
 fp16 output over xGMI.  Total work is fixed, so "scaling" is "strong".
 
 Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
-GEMM) and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
+linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
 forward, timed on a bounded sample on this host).
 """
 import argparse
@@ -20,6 +21,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -45,10 +47,15 @@ CONFIGS = {
 }
 
 
-def alg_bytes(M, N, K, abits):
-    """Algorithmic HBM bytes of one GEMM launch: packed W (0.75 B/w) + W scales
-    + int8 X + X scales + fp16 D."""
-    return N * K * 6 // 8 + 2 * N * K // GROUP + M * K + 2 * M * K // GROUP + 2 * M * N
+LINEARS = ("qkv", "o", "gate", "up", "down")
+
+
+def alg_bytes(M, N, K, abits, fused=True):
+    """Algorithmic HBM bytes of one linear launch: packed W (0.75 B/w) + W
+    scales (2 B per 128 weights, inside the weight image) + the activations + fp16 D.  Fused (decode) launches read fp16 x (2 B/elem) and quantize
+    in-kernel; unfused ones read int8 X + X scales (their quantize launch is bytes_quant)."""
+    act = 2 * M * K if fused else M * K + 2 * M * K // GROUP
+    return N * K * 6 // 8 + 2 * N * K // GROUP + act + 2 * M * N
 
 
 def build_stack(cfg, rank, world, dev, seed=1234):
@@ -58,15 +65,15 @@ def build_stack(cfg, rank, world, dev, seed=1234):
     for _ in range(layers):
         L = {}
         for (name, N, K, abits) in lins:
-            assert N % (32 * world) == 0, f"{name}: N={N} not divisible into 32-column shards for {world} ranks"
+            assert N % (16 * world) == 0, f"{name}: N={N} not divisible into 16-column shards for {world} ranks"
             Nl = N // world
             wq = torch.randint(-32, 32, (Nl, K), dtype=torch.int8, device=dev, generator=g)
-            pk = ops.pack_w6(wq)
-            del wq
             ws = (torch.rand((K // GROUP, Nl), device=dev, generator=g) * 0.02 + 1e-3).half()
+            pk = ops.pack_w6(wq, ws)  # the weight image: 6-bit codes + blocked group scales
+            del wq, ws
             out = torch.empty((M, Nl), dtype=torch.float16, device=dev)
             full = torch.empty((world * M * Nl,), dtype=torch.float16, device=dev) if world > 1 else None
-            L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, ws=ws, out=out, full=full)
+            L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full)
         # synthetic fp16 inputs of each linear (attention / activation outputs are out of scope)
         for name in ("qkv", "o", "gate", "down"):
             K = L[name]["K"]
@@ -75,32 +82,17 @@ def build_stack(cfg, rank, world, dev, seed=1234):
     return stack
 
 
-def run_step(stack, M, world, group=None, gemm_only=False, pre=None):
-    """One token through the linear stack.  pre: pre-quantized inputs for gemm_only."""
-    for li, L in enumerate(stack):
-        for name in ("qkv", "o", "gate", "up", "down"):
-            p = L[name]
-            src = "gate" if name == "up" else name
-            if gemm_only:
-                xq, xs = pre[li][src]
-            elif name != "up":
-                xq, xs = ops.quantize_act(L[src]["x"], p["abits"])
-                L["_q"] = (xq, xs)
-            else:
-                xq, xs = L["_q"]
-            ops.gemm_w6ax(xq, xs, p["pk"], p["ws"], p["Nl"], p["abits"], out=p["out"])
-            if world > 1 and not gemm_only:
-                dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
-
-
-def prequantize(stack):
-    pre = []
+def run_step(stack, M, world, group=None, gather=True):
+    """One token through the linear stack: fq_linear_w6ax per linear (decode sizes: one fused
+    quantize+GEMM launch each; gate and up read the same input), then one RCCL all-gather of the
+    fp16 shard outputs per linear when world > 1."""
     for L in stack:
-        d = {}
-        for name in ("qkv", "o", "gate", "down"):
-            d[name] = ops.quantize_act(L[name]["x"], L[name]["abits"])
-        pre.append(d)
-    return pre
+        for name in LINEARS:
+            p = L[name]
+            x = L["gate" if name == "up" else name]["x"]
+            ops.linear_w6ax(x, p["pk"], p["Nl"], p["abits"], out=p["out"])
+            if world > 1 and gather:
+                dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
 
 
 def capture(fn, stream):
@@ -119,6 +111,42 @@ def time_graph(g, reps, stream):
         e.record(stream)
     e.synchronize()
     return s.elapsed_time(e) / 1e3  # seconds
+
+
+NORTH_STAR_SHAPES = [(24576, 8192), (8192, 8192), (28672, 8192), (8192, 28672)]  # test_flexq_kernel.sh:25-28
+
+
+def fp16_compare(shapes, M, abits, dev, reps=20):
+    """North-star denominator: rocBLAS/hipBLASLt fp16 GEMM (torch F.linear, fp16 weights) vs the
+    W6Ax linear at the same (M, N, K).  Each side replays a graph of `reps` launches rotating over
+    enough weight copies (>= 768 MB) that the 256 MB MALL cannot serve them."""
+    out = []
+    g = torch.Generator(device=dev).manual_seed(7)
+    s = torch.cuda.Stream(dev)
+    for (N, K) in shapes:
+        x = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+        copies = max(2, -(-768 * 2**20 // (2 * N * K)))
+        w16 = [torch.randn((N, K), dtype=torch.float16, device=dev, generator=g) * 0.02 for _ in range(copies)]
+        y16 = torch.empty((M, N), dtype=torch.float16, device=dev)
+        wq = [ops.pack_w6(torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g),
+                          (torch.rand((K // GROUP, N), device=dev, generator=g) * 0.02).half()) for _ in range(copies)]
+        y6 = torch.empty((M, N), dtype=torch.float16, device=dev)
+        with torch.cuda.stream(s):  # eager warm-up (hipBLASLt heuristics, workspaces)
+            torch.nn.functional.linear(x, w16[0], out=y16)
+            ops.linear_w6ax(x, wq[0], N, abits, out=y6)
+        torch.cuda.synchronize()
+        g16 = capture(lambda: [torch.nn.functional.linear(x, w16[i % copies], out=y16) for i in range(reps)], s)
+        g6 = capture(lambda: [ops.linear_w6ax(x, wq[i % copies], N, abits, out=y6) for i in range(reps)], s)
+        for gr in (g16, g6):
+            gr.replay()
+        torch.cuda.synchronize()
+        t16 = time_graph(g16, 5, s) / (5 * reps)
+        t6 = time_graph(g6, 5, s) / (5 * reps)
+        out.append({"N": N, "K": K, "M": M, "fp16_us": round(t16 * 1e6, 2), "w6_us": round(t6 * 1e6, 2),
+                    "speedup": round(t16 / t6, 3)})
+        del g16, g6, w16, wq
+        torch.cuda.synchronize()
+    return out
 
 
 def cpu_baseline(budget_s=15.0):
@@ -161,6 +189,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline (0 = skip)")
     ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,18 +249,19 @@ def main():
     value = flops_step * a.steps / elapsed / 1e12
     tok_s = M * a.steps / elapsed
 
-    # roofline of the dominant kernel (the decode GEMM): a graph of the step's GEMM launches only
-    pre = prequantize(stack)
-    torch.cuda.synchronize()
-    g2 = capture(lambda: run_step(stack, M, world, gemm_only=True, pre=pre), stream)
+    # roofline of the dominant kernel (the fused decode linear): a graph of the step's linear
+    # launches only (no all-gather), timed with HIP events on the capture stream
+    g2 = capture(lambda: run_step(stack, M, world, gather=False), stream)
     for _ in range(2):
         g2.replay()
     torch.cuda.synchronize()
     t_g = time_graph(g2, a.roofline_reps, stream)
     launches = layers * len(lins)
     per_launch_s = t_g / (a.roofline_reps * launches)
-    bytes_launch = layers * sum(alg_bytes(M, N // world, K, ab) for (_, N, K, ab) in lins) / launches
+    fused = {(N, K): ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in lins}
+    bytes_launch = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)]) for (_, N, K, ab) in lins) / launches
     achieved = bytes_launch / per_launch_s / 1e9
+    del g2
 
     res = {
         "metric": "W6A6 GEMM TFLOPS-equiv + tok/s on LLaMA-2-7B linear shapes, 1/2/4/8 GPU",
@@ -255,7 +285,7 @@ def main():
             "graph": not a.no_graph,
         },
         "roofline": {
-            "kernel": "fq_gemm_decode_kernel",
+            "kernel": "fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else "fq_gemm_decode_kernel (+ quantize where unfused)",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -264,9 +294,23 @@ def main():
             "traffic": None,
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
-            "method": "graph of the step's GEMM launches only, HIP events on the capture stream",
+            "fused_launches": all(fused.values()),
+            "method": "graph of the step's linear launches only (no all-gather), HIP events on the capture stream",
         },
     }
+    if world == 1 and not a.no_fp16_compare:
+        del stack
+        torch.cuda.empty_cache()
+        shapes = sorted({(N, K) for (_, N, K, _) in lins})
+        cmp_cfg = fp16_compare(shapes, M, 6, dev)
+        cmp_ns = fp16_compare(NORTH_STAR_SHAPES, 1, 6, dev)
+        geo = lambda rows: round(float(np.exp(np.mean([np.log(r["speedup"]) for r in rows]))), 3)
+        res["vs_rocblas_fp16"] = {
+            "what": "W6A6 linear (fused quantize+GEMM) vs torch F.linear fp16 (hipBLASLt/rocBLAS), same M,N,K, graph-timed",
+            "config_shapes": cmp_cfg, "config_geomean_speedup": geo(cmp_cfg),
+            "llama2_70b_m1": cmp_ns, "llama2_70b_m1_geomean_speedup": geo(cmp_ns),
+            "north_star_target": 1.3,
+        }
     if rank == 0 and world == 1 and a.cpu_budget > 0:
         res["cpu_baseline"] = cpu_baseline(a.cpu_budget)
     if rank == 0:

@@ -42,15 +42,16 @@ _SIGS = {
     "fq_packed_w_bytes": ([I, I], SZ),
     "fq_gemm_workspace_bytes": ([I, I, I], SZ),
     "fq_workspace_init": ([P, SZ, P], I),
-    "fq_pack_w6": ([P, I, I, P, P], I),
-    "fq_unpack_w6": ([P, I, I, P, P], I),
+    "fq_pack_w6": ([P, P, I, I, P, P], I),
+    "fq_unpack_w6": ([P, I, I, P, P, P], I),
     "fq_quantize_pack_w6": ([P, I, I, P, P, P, P], I),
     "fq_quantize_act": ([P, I, I, I, P, P, P], I),
-    "fq_gemm_w6ax": ([P, P, P, P, I, I, I, I, P, P, P, SZ, P], I),
-    "fq_linear_w6ax": ([P, I, I, I, I, P, P, P, P, P, P, SZ, P], I),
+    "fq_gemm_w6ax": ([P, P, P, I, I, I, I, P, P, P, SZ, P], I),
+    "fq_linear_w6ax": ([P, I, I, I, I, P, P, P, P, P, SZ, P], I),
+    "fq_linear_act_scratch_bytes": ([I, I, I], SZ),
     "fq_ref_bit_packing": ([P, P, I, I, I, P], I),
     "fq_ref_quantize_bit_packing": ([P, P, P, I, I, I, P], I),
-    "fq_import_ref_w": ([P, I, I, P, P], I),
+    "fq_import_ref_w": ([P, P, I, I, P, P], I),
     "fq_import_ref_x": ([P, P, I, I, I, P, P, P], I),
     "fq_bmma_scratch_bytes": ([I, I, I], SZ),
 }

@@ -1,6 +1,10 @@
 // fq_api.hip -- remaining C-ABI entry points: info, fused linear, FQBMMA-style state API.
 #include "fq_common.h"
 
+fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
+                                 uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
+                                 hipStream_t s, bool *launched);
+
 extern "C" const char *fq_version(void) { return "flexq_amd 0.1.0 (gfx950, int8-MFMA W6Ax)"; }
 
 extern "C" const char *fq_status_string(fq_status s) {
@@ -16,13 +20,21 @@ extern "C" const char *fq_status_string(fq_status s) {
 }
 
 extern "C" fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits,
-                                    const void *w_packed, const uint16_t *ws, uint16_t *d,
+                                    const void *w_packed, uint16_t *d,
                                     int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                                     size_t workspace_bytes, fq_stream_t stream) {
+    if (!x || !w_packed || !d) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    // decode sizes: one launch, the quantizer runs inside the GEMM's prologue (xq/xs untouched)
+    bool launched = false;
+    fq_status st = fq_decode_linear_fused(x, M, N, K, abits, w_packed, d, nullptr, workspace,
+                                          workspace_bytes, (hipStream_t)stream, &launched);
+    if (launched || st != FQ_OK) return st;
     if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
-    fq_status st = fq_quantize_act(x, M, K, abits, xq_buf, xs_buf, stream);
+    st = fq_quantize_act(x, M, K, abits, xq_buf, xs_buf, stream);
     if (st != FQ_OK) return st;
-    return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, ws, M, N, K, abits, d, nullptr, workspace,
+    return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace,
                         workspace_bytes, stream);
 }
 
@@ -55,7 +67,9 @@ extern "C" fq_bmma_state fq_bmma_init(const int32_t *X, const void *W, const uin
     st.scratch_bytes = scratch_bytes;
     // Same acceptance rules as FQBMMAOp::initialize (flexq_bmma_op.h:81-133): group 128, no bias,
     // K % 128 == 0; plus this build's W6 / A{6,8} and the bit-plane row rule (M <= 8 or M % 8 == 0).
-    st.init_success = X && W && X_SCALE && W_SCALE && D && group_size == FQ_GROUP && !bias &&
+    // W is the weight image (fq_import_ref_w(W planes, W_SCALE) once, offline): it carries the
+    // group scales, so W_SCALE is kept for the signature and may be NULL.
+    st.init_success = X && W && X_SCALE && D && group_size == FQ_GROUP && !bias &&
                       M > 0 && N > 0 && K > 0 && K % FQ_GROUP == 0 && (M <= 8 || M % 8 == 0) &&
                       w_bits == 6 && (x_bits == 6 || x_bits == 8) && scratch &&
                       scratch_bytes >= fq_bmma_scratch_bytes(M, N, K);
@@ -70,6 +84,6 @@ extern "C" fq_status fq_bmma_exec(const fq_bmma_state *st, fq_stream_t stream) {
     void *ws = base + align256((size_t)st->M * st->K) + align256((size_t)st->M * (st->K / FQ_GROUP) * 2);
     fq_status s = fq_import_ref_x(st->X, st->X_SCALE, st->M, st->K, st->x_bits, xq, xs, stream);
     if (s != FQ_OK) return s;
-    return fq_gemm_w6ax(xq, xs, st->W, st->W_SCALE, st->M, st->N, st->K, st->x_bits, st->D, nullptr,
+    return fq_gemm_w6ax(xq, xs, st->W, st->M, st->N, st->K, st->x_bits, st->D, nullptr,
                         ws, fq_gemm_workspace_bytes(st->M, st->N, st->K), stream);
 }

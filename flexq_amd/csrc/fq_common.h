@@ -28,10 +28,76 @@ __device__ __forceinline__ float round_half_away(float v) {
 // CUDA's saturating float->int (cvt.rzi.s32.f32) followed by clamp(lo, hi):
 // NaN -> 0, +inf -> hi, -inf -> lo.
 __device__ __forceinline__ int sat_clamp(float v, int lo, int hi) {
-    if (v != v) return 0;
-    if (v >= (float)hi) return hi;
-    if (v <= (float)lo) return lo;
-    return (int)v;
+    const int c = (int)fminf(fmaxf(v, (float)lo), (float)hi);  // branch-free; exact in range
+    return v == v ? c : 0;
+}
+
+// ---- dynamic group quantizer (one 128-wide group over 16 consecutive, 16-aligned lanes) ----
+// Restates e2e .../flexqgemm/src/pack/bit_packing.cu:125-164 exactly: fp16 absmax seeded with
+// -1 (:139; fmaxf drops NaN like __hmax), maxv = absmax / (2^(b-1)-1) in IEEE fp32, scale =
+// half(maxv) round-to-nearest, q = clamp(roundf(float(x) / float(scale))) with CUDA's saturating
+// conversion.  `raw` = this lane's 8 fp16; all 16 lanes of the group must execute the call.
+// Returns the fp16 scale bits and the 8 codes packed as little-endian int8 bytes.
+//
+// The 16-lane max runs on DPP (quad_perm xor1/xor2, row_half_mirror, row_mirror: a full max
+// over the 16-lane row without LDS).  The per-element quotient x / s is v_rcp + one exact-FMA
+// Newton step instead of the IEEE division sequence; the codes are identical because x and s are
+// fp16 (11-bit significands): a quotient that is not exactly a half-integer k + 0.5 lies at least
+// 2^-12 relative away from one, far beyond the step's ~2^-23 error, and an exactly representable
+// quotient (ties included) is reproduced exactly by the Newton step.  Non-finite intermediates
+// (s = 0 or inf) take the plain product, which has the IEEE quotient's value class.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float max16(float m) {
+    m = fmaxf(m, dpp_f32<0xB1>(m));   // quad_perm [1,0,3,2]
+    m = fmaxf(m, dpp_f32<0x4E>(m));   // quad_perm [2,3,0,1]
+    m = fmaxf(m, dpp_f32<0x141>(m));  // row_half_mirror: quad q <-> quad 1-q within 8 lanes
+    m = fmaxf(m, dpp_f32<0x140>(m));  // row_mirror: half h <-> half 1-h within the 16-lane row
+    return m;
+}
+
+// v_cvt_i32_f32: truncation with the hardware's saturation (out of range clamps, NaN -> 0),
+// the same results as CUDA's cvt.rzi.s32.f32 that the reference relies on.
+__device__ __forceinline__ int cvt_i32_sat(float v) {
+    int r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
+__device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &codes) {
+    const uint16_t h[8] = {(uint16_t)raw.x, (uint16_t)(raw.x >> 16), (uint16_t)raw.y, (uint16_t)(raw.y >> 16),
+                           (uint16_t)raw.z, (uint16_t)(raw.z >> 16), (uint16_t)raw.w, (uint16_t)(raw.w >> 16)};
+    const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
+    float v[8];
+    float mx = -1.0f;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        v[i] = h2f(h[i]);
+        mx = fmaxf(mx, fabsf(v[i]));
+    }
+    mx = max16(mx);
+    const float maxv = mx / (float)hi;  // IEEE fp32 division (no fast-math in this build)
+    const uint16_t sh = f2h(maxv);
+    const float r = h2f(sh);
+    const float rc = __builtin_amdgcn_rcpf(r);
+    const bool newton = __builtin_isfinite(r) && r != 0.0f;  // else the plain product (inf/NaN class)
+    uint32_t w[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const float q1 = v[i] * rc;
+        const float q = newton ? fmaf(fmaf(-q1, r, v[i]), rc, q1) : q1;
+        // roundf = trunc(q + copysign(0.5, q)) here: q is either an exact half-integer or at
+        // least 2^-12 (relative) away from one, so the addition cannot cross an integer; the
+        // saturating conversion then maps +-inf to the int range and NaN to 0 (sat_clamp).
+        const int c = cvt_i32_sat(__builtin_truncf(q + __builtin_copysignf(0.5f, q)));
+        const int qc = min(max(c, lo), hi);  // v_med3_i32
+        w[i >> 2] |= (uint32_t)(qc & 255) << (8 * (i & 3));
+    }
+    codes = make_uint2(w[0], w[1]);
+    return sh;
 }
 
 // ---- fq6 weight unpack ----------------------------------------------------------------------

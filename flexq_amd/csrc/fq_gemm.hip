@@ -3,45 +3,18 @@
 // Contraction: the reference emulates INT6 x INT6 with 36 binary MMAs per bit-pair set
 // (mma.m8n8k128.b1.and.popc, engine/src/bgemm/bgemm.cuh:431-450).  Here a 6-bit weight is
 // unpacked in registers into the top 6 bits of an int8 (value 4w, fq_common.h unpack_fq6) and
-// the contraction runs on v_mfma_i32_32x32x32_i8 with int32 accumulation, reset every 128-wide
-// group.  acc4 = 4 * sum_k x*w exactly (|acc4| <= 2^21), so float(acc4) is exact and the final
-// x0.25 is exact: the result equals sum_g float(half(xs*ws)) * acc_g accumulated in fp32,
-// which is the reference's dequant (flexq_bmma_kernel.h:359-373) with the bit-pair sum moved
-// inside the integer accumulator.
+// the contraction runs on v_mfma_i32_16x16x64_i8 with int32 accumulation, reset every 128-wide
+// group (two k-steps of 64).  acc4 = 4 * sum_k x*w exactly (|acc4| <= 2^21), so float(acc4) is
+// exact and the final x0.25 is exact: the result equals sum_g float(half(xs*ws)) * acc_g
+// accumulated in fp32, which is the reference's dequant (flexq_bmma_kernel.h:359-373) with the
+// bit-pair sum moved inside the integer accumulator.
 //
-// MFMA operand maps (32x32x32 i8): lane l holds A[row l&31][k = 16*(l>>5) + j] and
-// B[k = 16*(l>>5) + j][col l&31], j = 0..15 -- any k relabelling shared by A and B gives the same
-// sum; C/D: col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5) (dtype-independent on gfx950).
+// MFMA operand maps (16x16x64 i8): lane l holds A[row l&15][k = 16*(l>>4) + j] and
+// B[k = 16*(l>>4) + j][col l&15], j = 0..15 -- any k relabelling shared by A and B gives the same
+// sum; C/D: col = l&15, row = 4*(l>>4) + r, r = 0..3 (cdna_hip_programming.md §3).  The fq6
+// weight layout stores exactly these B operands (16-column tiles, fq_quant.hip).
 #include "fq_common.h"
 
-__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
-
-// Valid accumulator registers for a row tile of MT rows (rows >= MT are never stored).
-template <int MT> struct RowRegs { static constexpr int RV = MT <= 8 ? 4 : (MT <= 16 ? 8 : 16); };
-
-// =============================================================================================
-// Decode / small-M kernel (M <= 32): HBM-bound weight streaming.
-//
-// Work items are (n-tile t of 32 columns, k-split z).  A workgroup (one per CU, persistent over
-// items w, w + grid, ...) streams each item's contiguous fq6 blocks (3 KiB = 32 columns x one
-// 128-wide group); its NW waves take contiguous group sub-ranges, so a tile's partial sums meet
-// in LDS (one barrier per item) and S = 1 needs no cross-CU reduction.  Measured on MI355X
-// (tools/ubench_stream.hip): one CU streams at most ~50 GB/s while the chip reaches ~6.5 TB/s,
-// so whole tiles per CU keep the chip at the aggregate limit; only small N (tensor-parallel
-// shards) split K (S > 1, one item per WG).
-//   * Ring: D weight slots per wave filled by LDS-DMA (global_load_lds_dwordx4 nt, three 1 KiB
-//     planes per block), retired by hand-counted `s_waitcnt vmcnt(U * in-flight)`, and running
-//     ahead across item boundaries.  LDS reads are inline asm (hipcc would guard them with
-//     vmcnt(0) against the in-flight DMA); the per-item barrier is a raw s_barrier (a
-//     __syncthreads() would drain the ring).
-//   * Staging (XS/SS = 0): a few wide LDS-DMA instructions in the prologue stage the blocks'
-//     w-scales / x-scales and (M <= 4) activation rows, so the loop moves weights only.  When the
-//     staged bytes would not fit LDS (very long K), they ride in each ring slot instead (XS/SS = 1).
-//   * S > 1: the WG publishes its fp32 partial tile with write-through (sc1) stores, drains them,
-//     takes one agent-scope ticket, and the last WG of the tile sums the S slabs in z order
-//     (sc1 loads, all in flight together).  Deterministic: fixed order, no float atomics.
-//     (MI355X_MICROARCH.md "Valid forms", row 1.)
-// =============================================================================================
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
@@ -52,69 +25,161 @@ __device__ __forceinline__ v4i ds_read_b128(uint32_t a) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
     return v;
 }
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2u ds_read_b64(uint32_t a) {
+    v2u v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ void ds_write_b64(uint32_t a, uint2 v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ds_write_b32(uint32_t a, uint32_t v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
 __device__ __forceinline__ uint32_t ds_read_u16(uint32_t a) {
     uint32_t v;
     asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(a));
     return v;
 }
 
-template <int U>
+template <int U, int D>
 __device__ __forceinline__ void wait_ring(int later) {
-    // s_waitcnt takes an immediate: `later` blocks (U DMA instructions each) may stay in flight
-    switch (later) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(U) : "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * U) : "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * U) : "memory"); break;
+    // s_waitcnt takes an immediate: `later` (< D) blocks of U DMA instructions may stay in flight
+#define FQ_WAIT_CASE(k)                                                                 \
+    if constexpr (D > (k)) {                                                            \
+        if (later == (k)) {                                                             \
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"((k) * U) : "memory");              \
+            return;                                                                     \
+        }                                                                               \
     }
+    FQ_WAIT_CASE(11) FQ_WAIT_CASE(10) FQ_WAIT_CASE(9) FQ_WAIT_CASE(8) FQ_WAIT_CASE(7) FQ_WAIT_CASE(6)
+    FQ_WAIT_CASE(5) FQ_WAIT_CASE(4) FQ_WAIT_CASE(3) FQ_WAIT_CASE(2) FQ_WAIT_CASE(1)
+#undef FQ_WAIT_CASE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// XS: activation rows staged (0, M <= 4 only) or carried per ring slot (1).
+// Activation rows in LDS are 128 B (one group) with their eight 16-byte chunks XOR-swizzled by
+// (row & 7): the A-operand read (16 rows x 16 B per k-chunk) is then conflict-free per 8 lanes.
+__host__ __device__ inline int xswz(int row, int chunk) { return (chunk ^ (row & 7)) * 16; }
+
+// =============================================================================================
+// Decode / small-M kernel (M <= 32): HBM-bound weight streaming.
+//
+// Work items are (n-tile t of 16 columns, k-split z).  A workgroup (one per CU, persistent over
+// items w, w + grid, ...) streams each item's contiguous fq6 blocks (1.5 KiB = 16 columns x one
+// 128-wide group); its NW waves take contiguous group sub-ranges, so a tile's partial sums meet
+// in LDS and S = 1 needs no cross-CU reduction.  Measured on MI355X (tools/stamps.py): a CU
+// streams ~24 GB/s when the whole chip streams, so the per-CU work must be even -- 16-column
+// tiles make the LLaMA widths (4096 k) divide evenly over 256 CUs, and a cross-CU split-K
+// fix-up (~1.2 us) is reserved for narrow N (tensor-parallel shards).
+//   * Ring: D weight slots per wave filled by LDS-DMA (global_load_lds_dwordx4 nt: one 1 KiB and
+//     one 512 B instruction per block), retired by hand-counted `s_waitcnt vmcnt(U * in-flight)`,
+//     running ahead across item boundaries.  LDS reads are inline asm (hipcc would guard them
+//     with vmcnt(0) against the in-flight DMA); item-end barriers are raw s_barrier (a
+//     __syncthreads() would drain the ring).
+//   * Staging (XS/SS = 0): a few wide LDS-DMA instructions in the prologue stage the blocks'
+//     w-scales / x-scales and the activation rows, so the loop moves weights only.  When the
+//     staged bytes would not fit LDS (very long K), they ride in each ring slot instead (XS/SS = 1).
+//   * FUSE: the kernel quantizes the fp16 activations itself (see below).
+//   * S > 1: each item's fp32 partial tile goes out with write-through (sc1) stores; after the
+//     loop the WG drains them once, takes one agent-scope ticket per item, and the last WG of a
+//     tile sums the S slabs in z order (sc1 loads, 8 in flight).  Deterministic: fixed order,
+//     no float atomics.  (MI355X_MICROARCH.md "Valid forms", row 1.)
+// =============================================================================================
+constexpr int FQ_BLOCK = 1536;  // bytes of one (16-column tile, group) fq6 block
+
+// waves per WG (one WG per CU): 8, or 4 for 32-row tiles (their reduction buffers are larger)
+#ifndef FQ_DECODE_WAVES
+#define FQ_DECODE_WAVES 8
+#endif
+__host__ __device__ constexpr int decode_waves(int MT) { return MT <= 16 ? FQ_DECODE_WAVES : FQ_DECODE_WAVES / 2; }
+// ring depth: up to 8 slots within a per-wave ring budget of 16 KiB (8 waves) / 32 KiB (4 waves),
+// halved when M > 4 rows of activations are staged (they take the LDS instead)
+#ifndef FQ_RING_BUDGET
+#define FQ_RING_BUDGET 4608
+#endif
+#ifndef FQ_RING_DMAX
+#define FQ_RING_DMAX 3
+#endif
+__host__ __device__ constexpr int decode_ring_budget(int MT, int XS) {
+    return (decode_waves(MT) == 8 ? FQ_RING_BUDGET : 2 * FQ_RING_BUDGET) / (XS == 0 && MT > 4 ? 2 : 1);
+}
+__host__ __device__ constexpr int decode_depth_cap(int U) { return 63 / U + 1 < FQ_RING_DMAX ? 63 / U + 1 : FQ_RING_DMAX; }
+__host__ __device__ constexpr int decode_depth_for(int MT, int XS, int slot, int U) {
+    // (D - 1) * U must fit the 6-bit vmcnt immediate; at least 2 slots
+    return decode_ring_budget(MT, XS) / slot < 2 ? 2
+           : decode_ring_budget(MT, XS) / slot < decode_depth_cap(U) ? decode_ring_budget(MT, XS) / slot
+                                                                     : decode_depth_cap(U);
+}
+
+// XS: activation rows staged for the wave's groups (0) or carried per ring slot (1).
 // SS: w-/x-scales staged (0) or carried per ring slot (1).
-// A sub-dword LDS-DMA writes lane l's value zero-extended to dword l of the destination.
+// XSR: x-scale record per group in LDS (dwords; rows >= M are read but never used).
 template <int MT, int XS, int SS> struct DecodeCfg {
+    static constexpr int RG = MT <= 16 ? 1 : 2;                  // 16-row MFMA row groups
+    static constexpr int XSR = 16 * RG;
     static constexpr int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;  // 1 KiB activation pieces per slot
-    static constexpr int WS_OFF = 3072 + XP * 1024;              // slot scales (SS = 1): 32 + MT dwords
-    static constexpr int XS_OFF = WS_OFF + 128;
-    static constexpr int SLOT = SS ? XS_OFF + MT * 4 : WS_OFF;
-    static constexpr int U = 3 + XP + (SS ? 2 : 0);              // ring DMA instructions per block
-    static constexpr int D = MT <= 4 ? 4 : (MT <= 16 ? 3 : 2);   // ring depth
+    static constexpr int WS_OFF = FQ_BLOCK + XP * 1024;         // slot scales (SS = 1)
+    static constexpr int XS_OFF = WS_OFF + 64;
+    static constexpr int SLOT = SS ? XS_OFF + XSR * 4 : WS_OFF;
+    static constexpr int U = 2 + XP + (SS ? 2 : 0);              // ring DMA instructions per block
+    static constexpr int D = decode_depth_for(MT, XS, SLOT, U);   // ring depth
 };
 
+__host__ __device__ inline int decode_xsr(int MT) { return MT <= 16 ? 16 : 32; }
 __host__ __device__ inline int decode_slot(int MT, int XS, int SS) {
     const int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;
-    return SS ? 3072 + XP * 1024 + 128 + MT * 4 : 3072 + XP * 1024;
+    return SS ? FQ_BLOCK + XP * 1024 + 64 + decode_xsr(MT) * 4 : FQ_BLOCK + XP * 1024;
 }
-__host__ __device__ inline int decode_depth(int MT) { return MT <= 4 ? 4 : (MT <= 16 ? 3 : 2); }
+
 // staged regions, rounded up to whole DMA instructions (each writes 64 lanes' worth)
-__host__ __device__ inline int decode_wsst_bytes(int nb, bool even) { return even ? ((nb + 3) / 4) * 256 : ((nb + 1) / 2) * 256; }
-__host__ __device__ inline int decode_xsst_bytes(int ng, int MT) { return ((ng * MT + 63) / 64) * 256; }
-__host__ __device__ inline int decode_xst_bytes(int ng, int M) {
-    const int per = 64 / (8 * M);
-    return ((ng + per - 1) / per) * per * M * 128;
-}
-// per-wave LDS: [ring D x SLOT][ws: nb x (16|32) dwords][xs: ng x MT dwords][x: ng x M x 128 B]
-__host__ __device__ inline int decode_wave_lds(int MT, int XS, int SS, int ng, int nb, int M, bool even) {
-    int b = decode_depth(MT) * decode_slot(MT, XS, SS);
-    if (!SS) b += decode_wsst_bytes(nb, even) + decode_xsst_bytes(ng, MT);
+__host__ __device__ inline int decode_wsst_bytes(int nb) { return ((nb + 31) / 32) * 1024; }
+__host__ __device__ inline int decode_xsst_bytes(int ng, int MT) { return ((ng * decode_xsr(MT) + 63) / 64) * 256; }
+__host__ __device__ inline int decode_xst_bytes(int ng, int M) { return ((ng * M + 7) / 8) * 1024; }
+// fused quantizer: fp16 window of xwin (group, row) pairs (a multiple of 4, at most 32 = 8 KiB)
+__host__ __device__ inline int decode_xwin_bytes(int ng, int M, int xwin) { return (ng * M < xwin ? (ng * M + 3) / 4 * 4 : xwin) * 256; }
+// per-wave LDS: [ring D x SLOT][ws: nb x 8 dwords][xs: ng x XSR dwords][x: ng x M x 128 B]
+//               [FUSE: fp16 window]
+__host__ __device__ inline int decode_wave_lds(int MT, int XS, int SS, int ng, int nb, int M, int xwin) {
+    const int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;
+    int b = decode_depth_for(MT, XS, decode_slot(MT, XS, SS), 2 + XP + (SS ? 2 : 0)) * decode_slot(MT, XS, SS);
+    if (!SS) b += decode_wsst_bytes(nb) + decode_xsst_bytes(ng, MT);
     if (!XS) b += decode_xst_bytes(ng, M);
+    if (xwin) b += decode_xwin_bytes(ng, M, xwin);
     return b;
 }
 
-template <int MT, int NW, int XS, int SS, bool DBG, int ABL = 0>
-__global__ __launch_bounds__(NW * 64) void fq_gemm_decode_kernel(
-    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk,
-    const uint16_t *__restrict__ ws, int M, int N, int K, uint16_t *__restrict__ d,
-    int32_t *__restrict__ acc_dbg, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW) {
+#ifdef FQ_DEV_ABLATION
+// development timeline: per WG (wave 0) s_memrealtime stamps (100 MHz), tools/stamps.py
+__device__ unsigned long long g_fq_stamps[1024 * 8];
+#define FQ_STAMP(k)                                                                  \
+    if ((ABL & 16) && threadIdx.x == 0 && blockIdx.x < 1024) {                       \
+        g_fq_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
+    }
+#else
+#define FQ_STAMP(k)
+#endif
+
+// FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
+// group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
+// into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
+    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
+    const uint32_t *__restrict__ wpk, int M, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
+    float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin) {
     using C = DecodeCfg<MT, XS, SS>;
-    constexpr int D = C::D, RV = RowRegs<MT>::RV;
+    constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
+    static_assert(!FUSE || (XS == 0 && SS == 0), "fused quantization stages into LDS");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
+    FQ_STAMP(0);
+    const int G = K / FQ_GROUP, NT = (N + 15) / 16;
     const int items = NT * S;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nit = (items - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1
-    // k-split z is the same for all of this WG's items (S == 1, or one item per WG)
+    // k-split z is the same for all of this WG's items (the grid is a multiple of S)
     const int z = (int)blockIdx.x % S;
     const int gz0 = (int)((long)z * G / S), gz1 = (int)((long)(z + 1) * G / S);
     const int Gz = gz1 - gz0;
@@ -122,48 +187,73 @@ __global__ __launch_bounds__(NW * 64) void fq_gemm_decode_kernel(
     const int ga = gz0 + (int)((long)wid * Gz / NW), gb = gz0 + (int)((long)(wid + 1) * Gz / NW);
     const int ng = gb - ga;  // groups per item for this wave (may be 0)
     const int n = ng * nit;  // blocks in this wave's sequence
-    const bool even = (N & 1) == 0;  // w-scale rows are dword aligned: 4 blocks per staging DMA
+    // blocked w-scales of the image: fp16 [NT][G][16] after the weight blocks (fq_quant.hip)
+    const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
 
-    const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, even);
+    const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, FUSE ? xwin : 0);
     char *ring = smem + wid * wl;
-    char *ws_st = ring + D * C::SLOT;                                       // staged w-scales
-    char *xs_st = ws_st + (SS ? 0 : decode_wsst_bytes(ngmax * IPW, even));  // staged x-scales
-    char *x_st = xs_st + (SS ? 0 : decode_xsst_bytes(ngmax, MT));           // staged activations
-    const int EM = M * 32;                                                  // live elements of a tile
-    float *red = reinterpret_cast<float *>(smem + NW * wl);                 // [2][NW][M*32]
-    int *flag = reinterpret_cast<int *>(red + 2 * NW * EM);
+    char *ws_st = ring + D * C::SLOT;                                 // staged w-scales
+    char *xs_st = ws_st + (SS ? 0 : decode_wsst_bytes(ngmax * IPW));  // staged x-scales
+    char *x_st = xs_st + (SS ? 0 : decode_xsst_bytes(ngmax, MT));     // staged activations
+    const int EM = M * 16;                                            // live elements of a tile
+    float *red = reinterpret_cast<float *>(smem + NW * wl);           // [RC][NW][M*16]
+    int *flag = reinterpret_cast<int *>(red + RC * NW * EM);          // [IPW]
 
     auto item_tile = [&](int it) { return ((int)blockIdx.x + it * (int)gridDim.x) / S; };
 
-    if (n > 0 && !SS && !(ABL & 8)) {  // ---- prologue staging (issued first: the ring waits retire it in order)
-        if (even) {
-            for (int i0 = 0; i0 < n; i0 += 4) {  // w-scales: 4 blocks per instruction, 2 columns per lane
-                const int i = i0 + (lane >> 4) < n ? i0 + (lane >> 4) : n - 1;
-                const int col = 32 * item_tile(i / ng) + 2 * (lane & 15);
-                __builtin_amdgcn_global_load_lds(ws + (long)(ga + i % ng) * N + (col < N ? col : N - 2),
-                                                 LDS_PTR(ws_st + i0 * 64), 4, 0, 0);
-            }
-        } else {
-            for (int i0 = 0; i0 < n; i0 += 2) {  // w-scales: 2 blocks per instruction, ushort per lane
-                const int i = i0 + (lane >> 5) < n ? i0 + (lane >> 5) : n - 1;
-                const int col = 32 * item_tile(i / ng) + (lane & 31);
-                __builtin_amdgcn_global_load_lds(ws + (long)(ga + i % ng) * N + (col < N ? col : N - 1),
-                                                 LDS_PTR(ws_st + i0 * 128), 2, 0, 0);
+    // Fused quantizer.  The fp16 activations of the wave's (group, row) pairs come in by LDS-DMA
+    // (one 1 KiB instruction per 4 pairs) into a window of xwin pairs, issued ahead of the ring
+    // so that waiting for them does not wait for the ring; 16 lanes quantize one pair.
+    const int qsub = lane & 15;
+    const int R = ng * M;  // (group, row) pairs this wave quantizes
+    char *xh_st = x_st + (XS ? 0 : decode_xst_bytes(ngmax, M));  // fp16 window (FUSE)
+    auto x_fetch = [&](int r0) {  // pairs [r0, r0 + xwin) -> xh_st
+        for (int c = 0; c < xwin && r0 + c < R; c += 4) {
+            int rg = r0 + c + (lane >> 4);
+            rg = rg < R ? rg : R - 1;
+            const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+            __builtin_amdgcn_global_load_lds(xh + (long)row * K + (long)(ga + j) * FQ_GROUP + qsub * 8,
+                                             LDS_PTR(xh_st + c * 256), 16, 0, 0);
+        }
+    };
+    auto x_quant = [&](int r0) {
+        for (int c = 0; c < xwin && r0 + c < R; c += 4) {  // wave-uniform bounds
+            const int rg = r0 + c + (lane >> 4);
+            const v4i raw = ds_read_b128(lds_addr(xh_st + c * 256 + lane * 16));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);  // no use of `raw` may move above the wait
+            uint2 codes;
+            const uint16_t sh = quant_group16(make_uint4(raw[0], raw[1], raw[2], raw[3]), abits, codes);
+            if (rg < R) {
+                const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+                ds_write_b64(lds_addr(x_st + rg * 128 + xswz(row, qsub >> 1) + (qsub & 1) * 8), codes);
+                if (qsub == 0) ds_write_b32(lds_addr(xs_st + (j * XSR + row) * 4), sh);
             }
         }
-        for (int i0 = 0; i0 < ng; i0 += 64 / MT) {  // x-scales: MT per group, ushort per lane
-            const int i = i0 + lane / MT, row = lane % MT;
-            __builtin_amdgcn_global_load_lds(xs + (long)(ga + (i < ng ? i : ng - 1)) * M + (row < M ? row : M - 1),
-                                             LDS_PTR(xs_st + i0 * MT * 4), 2, 0, 0);
+    };
+
+    if (n > 0 && !SS && !(ABL & 8)) {  // ---- prologue staging (issued first: the ring waits retire it in order)
+        for (int i0 = 0; i0 < n; i0 += 32) {  // w-scales: 32 blocks (32 B = 2 lanes each) per instruction
+            const int i = i0 + (lane >> 1) < n ? i0 + (lane >> 1) : n - 1;
+            __builtin_amdgcn_global_load_lds(wsb + ((long)item_tile(i / ng) * G + ga + i % ng) * 16 + 8 * (lane & 1),
+                                             LDS_PTR(ws_st + i0 * 32), 16, 0, 0);
+        }
+        if (!FUSE) {
+            for (int i0 = 0; i0 < ng; i0 += 64 / XSR) {  // x-scales: XSR per group, ushort per lane
+                const int i = i0 + lane / XSR, row = lane % XSR;
+                __builtin_amdgcn_global_load_lds(xs + (long)(ga + (i < ng ? i : ng - 1)) * M + (row < M ? row : M - 1),
+                                                 LDS_PTR(xs_st + i0 * XSR * 4), 2, 0, 0);
+            }
         }
     }
-    if (n > 0 && !XS && !(ABL & 8)) {  // activation rows: 8 lanes x 16 B per row and group
-        const int per = 64 / (8 * M);
-        for (int i0 = 0; i0 < ng; i0 += per) {
-            const int i = i0 + lane / (8 * M), row = (lane / 8) % M;
-            if (lane < per * 8 * M)
-                __builtin_amdgcn_global_load_lds(xq + (long)row * K + (long)(ga + (i < ng ? i : ng - 1)) * FQ_GROUP + (lane & 7) * 16,
-                                                 LDS_PTR(x_st + i0 * M * 128), 16, 0, 0);
+    FQ_STAMP(7);
+    if (n > 0 && !XS && !FUSE && !(ABL & 8)) {  // activation rows: 8 lanes x 16 B per (group, row)
+        for (int r0 = 0; r0 < R; r0 += 8) {
+            const int rg = r0 + (lane >> 3) < R ? r0 + (lane >> 3) : R - 1;
+            const int j = rg / M, row = rg - j * M;
+            const int chunk = (lane & 7) ^ (row & 7);  // lands at position lane & 7 (xswz)
+            __builtin_amdgcn_global_load_lds(xq + (long)row * K + (long)(ga + j) * FQ_GROUP + chunk * 16,
+                                             LDS_PTR(x_st + r0 * 128), 16, 0, 0);
         }
     }
 
@@ -172,167 +262,207 @@ __global__ __launch_bounds__(NW * 64) void fq_gemm_decode_kernel(
     auto issue = [&](int i, int slot) {
         const int t = item_tile(i / ng), g = ga + i % ng;
         char *dst = ring + slot * C::SLOT;
-        const char *src = wbytes + ((long)t * G + g) * 3072;
+        const char *src = wbytes + ((long)t * G + g) * FQ_BLOCK;
+        __builtin_amdgcn_global_load_lds(src, LDS_PTR(dst), 16, 0, 2 /*nt*/);
+        if (lane < 32) __builtin_amdgcn_global_load_lds(src + 1024, LDS_PTR(dst + 1024), 16, 0, 2);
 #pragma unroll
-        for (int r = 0; r < 3; r++)
-            __builtin_amdgcn_global_load_lds(src + r * 1024, LDS_PTR(dst + r * 1024), 16, 0, 2 /*nt*/);
-#pragma unroll
-        for (int p = 0; p < C::XP; p++) {  // activation rows, 16 B per lane, row-major [MT][128]
-            const int c = p * 64 + lane, row = c >> 3;
-            __builtin_amdgcn_global_load_lds(xq + (long)(row < M ? row : M - 1) * K + (long)g * FQ_GROUP + (c & 7) * 16,
-                                             LDS_PTR(dst + 3072 + p * 1024), 16, 0, 0);
+        for (int p = 0; p < C::XP; p++) {  // activation rows [MT][128 B], swizzled chunks
+            const int row = p * 8 + (lane >> 3), chunk = (lane & 7) ^ (row & 7);
+            __builtin_amdgcn_global_load_lds(xq + (long)(row < M ? row : M - 1) * K + (long)g * FQ_GROUP + chunk * 16,
+                                             LDS_PTR(dst + FQ_BLOCK + p * 1024), 16, 0, 0);
         }
-        if (SS) {  // 32 w-scales (ushort, lanes 0..31) and MT x-scales (ushort, lanes 0..MT-1)
-            if (lane < 32) {
-                const int col = 32 * t + lane;
-                __builtin_amdgcn_global_load_lds(ws + (long)g * N + (col < N ? col : N - 1), LDS_PTR(dst + C::WS_OFF), 2, 0, 0);
-            }
-            if (lane < MT)
+        if (SS) {  // 16 w-scales (16 B per lane, lanes 0..1) and XSR x-scales (ushort, lanes 0..XSR-1)
+            if (lane < 2)
+                __builtin_amdgcn_global_load_lds(wsb + ((long)t * G + g) * 16 + 8 * lane, LDS_PTR(dst + C::WS_OFF), 16, 0, 0);
+            if (lane < XSR)
                 __builtin_amdgcn_global_load_lds(xs + (long)g * M + (lane < M ? lane : M - 1), LDS_PTR(dst + C::XS_OFF), 2, 0, 0);
         }
     };
-    const int pro = n < D ? n : D;
-    for (int i = 0; i < pro; i++) issue(i, i);
+    // Order: staging (above) -> first activation window -> exactly D ring issues (unrolled; slots
+    // past a short sequence get a never-read copy of its last block).  Waiting for the window is
+    // then `vmcnt(D*U)`: everything younger is the ring.  (Each wave instruction costs the CU's
+    // address unit ~30 cycles whatever its size, so only instructions that carry data are issued.)
+    if (FUSE && n > 0) x_fetch(0);
+    if (n > 0) {
+#pragma unroll
+        for (int i = 0; i < D; i++) issue(i < n ? i : n - 1, i);
+    }
+    FQ_STAMP(1);
 
-    const int arow = (lane & 31) < M ? (lane & 31) : M - 1;  // rows >= M mirror row M-1 (unused)
-    const int Npad = NT * 32;
+    if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(D * C::U) : "memory");
+        FQ_STAMP(5);
+        x_quant(0);
+        FQ_STAMP(6);
+        for (int r0 = xwin; r0 < R; r0 += xwin) {  // M > 4 or long K: later windows
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous window was read
+            x_fetch(r0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            x_quant(r0);
+        }
+    }
+
+    int arow[RG];  // A-operand rows (rows >= M mirror row M-1, never stored)
+#pragma unroll
+    for (int rg = 0; rg < RG; rg++) arow[rg] = 16 * rg + (lane & 15) < M ? 16 * rg + (lane & 15) : M - 1;
+    const int Npad = NT * 16;
     int i = 0;  // position in the wave's block sequence
     for (int it = 0; it < nit; it++) {
         const int t = item_tile(it);
-        const int col = 32 * t + (lane & 31);
-        float cur[16];
+        const int col = 16 * t + (lane & 15);
+        float cur[RG][4];
 #pragma unroll
-        for (int r = 0; r < 16; r++) cur[r] = 0.f;
+        for (int rg = 0; rg < RG; rg++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) cur[rg][r] = 0.f;
         for (int j = 0; j < ng; j++, i++) {
             const int g = ga + j, slot = i % D;
             const int later = (n - 1 - i) < (D - 1) ? (n - 1 - i) : (D - 1);
-            wait_ring<C::U>(later);  // this slot (and every older DMA, the staging included) landed
+            wait_ring<C::U, D>(later);  // this slot (and every older DMA, the staging included) landed
+            if (i == 0) FQ_STAMP(2);
             const uint32_t sp = lds_addr(ring + slot * C::SLOT);
-            const v4i p0 = ds_read_b128(sp + lane * 16);
-            const v4i p1 = ds_read_b128(sp + 1024 + lane * 16);
-            const v4i p2 = ds_read_b128(sp + 2048 + lane * 16);
-            v4i a[4];
-            const uint32_t xap = XS ? sp + 3072 + arow * FQ_GROUP + 16 * (lane >> 5)
-                                    : lds_addr(x_st + (j * M + arow) * FQ_GROUP + 16 * (lane >> 5));
+            const v2u p0 = ds_read_b64(sp + lane * 8);
+            const v2u p1 = ds_read_b64(sp + 512 + lane * 8);
+            const v2u p2 = ds_read_b64(sp + 1024 + lane * 8);
+            v4i a[RG][2];
 #pragma unroll
-            for (int s = 0; s < 4; s++) a[s] = ds_read_b128(xap + 32 * s);
-            const uint32_t wsa = SS ? sp + C::WS_OFF + 4 * (lane & 31)
-                                    : lds_addr(ws_st) + (even ? i * 64 + 2 * (lane & 31) : i * 128 + 4 * (lane & 31));
+            for (int rg = 0; rg < RG; rg++) {
+                const uint32_t xrow = XS ? sp + FQ_BLOCK + arow[rg] * FQ_GROUP
+                                         : lds_addr(x_st + (j * M + arow[rg]) * FQ_GROUP);
+#pragma unroll
+                for (int s = 0; s < 2; s++) a[rg][s] = ds_read_b128(xrow + xswz(arow[rg], 4 * s + (lane >> 4)));
+            }
+            const uint32_t wsa = (SS ? sp + C::WS_OFF : lds_addr(ws_st) + i * 32) + 2 * (lane & 15);
             const uint32_t wsv = ds_read_u16(wsa);
-            v4i xd[RV / 4];  // x-scales of rows 8q+4h .. +3, one per dword
-            const uint32_t xsa = SS ? sp + C::XS_OFF : lds_addr(xs_st + j * MT * 4);
+            v4i xd[RG];  // x-scales of rows 16rg + 4(lane>>4) .. +3, one per dword
+            const uint32_t xsa = SS ? sp + C::XS_OFF : lds_addr(xs_st + j * XSR * 4);
 #pragma unroll
-            for (int q = 0; q < RV / 4; q++) xd[q] = ds_read_b128(xsa + 4 * (8 * q + 4 * (lane >> 5)));
+            for (int rg = 0; rg < RG; rg++) xd[rg] = ds_read_b128(xsa + 4 * (16 * rg + 4 * (lane >> 4)));
             // every read has landed, and the slot's bytes are in registers before its refill
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             if (i + D < n) issue(i + D, slot);
 
             if (ABL & 2) {
-                cur[0] += (float)(p0[0] ^ p1[1] ^ p2[2] ^ a[3][0]) + (float)wsv + (float)xd[0][0];
+                cur[0][0] += (float)(p0[0] ^ p1[1] ^ p2[0] ^ a[0][1][0]) + (float)wsv + (float)xd[0][0];
                 continue;
             }
-            v16i acc = {0};
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], unpack_fq6(p0[s], p1[s], p2[s]), acc, 0, 0, 0);
+            const v4i b0 = unpack_fq6(p0[0], p1[0], p2[0]), b1 = unpack_fq6(p0[1], p1[1], p2[1]);
             const __half2 w2 = __half2half2(__ushort_as_half((uint16_t)wsv));
 #pragma unroll
-            for (int q = 0; q < RV / 4; q++) {  // rows 8q+4h .. +3
-                const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)xd[q][1], (uint32_t)xd[q][0], 0x05040100u);
-                const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)xd[q][3], (uint32_t)xd[q][2], 0x05040100u);
+            for (int rg = 0; rg < RG; rg++) {
+                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][0], b0, v4i{0, 0, 0, 0}, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][1], b1, acc, 0, 0, 0);
+                const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)xd[rg][1], (uint32_t)xd[rg][0], 0x05040100u);
+                const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)xd[rg][3], (uint32_t)xd[rg][2], 0x05040100u);
                 const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&x01), w2);  // fp16-rounded
                 const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&x23), w2);  // scale product
-                cur[4 * q + 0] = fmaf((float)acc[4 * q + 0], __low2float(p01), cur[4 * q + 0]);
-                cur[4 * q + 1] = fmaf((float)acc[4 * q + 1], __high2float(p01), cur[4 * q + 1]);
-                cur[4 * q + 2] = fmaf((float)acc[4 * q + 2], __low2float(p23), cur[4 * q + 2]);
-                cur[4 * q + 3] = fmaf((float)acc[4 * q + 3], __high2float(p23), cur[4 * q + 3]);
-            }
-            if (DBG) {
+                cur[rg][0] = fmaf((float)acc[0], __low2float(p01), cur[rg][0]);
+                cur[rg][1] = fmaf((float)acc[1], __high2float(p01), cur[rg][1]);
+                cur[rg][2] = fmaf((float)acc[2], __low2float(p23), cur[rg][2]);
+                cur[rg][3] = fmaf((float)acc[3], __high2float(p23), cur[rg][3]);
+                if (DBG) {
 #pragma unroll
-                for (int r = 0; r < RV; r++) {
-                    const int row = acc_row(r, lane);
-                    if (row < M && col < N) acc_dbg[((long)row * N + col) * G + g] = acc[r] >> 2;
+                    for (int r = 0; r < 4; r++) {
+                        const int row = 16 * rg + 4 * (lane >> 4) + r;
+                        if (row < M && col < N) acc_dbg[((long)row * N + col) * G + g] = acc[r] >> 2;
+                    }
                 }
             }
         }
 
-        // ---- item end: fixed-order reduction of the NW waves' partial tiles through LDS
-        // (raw s_barrier: the ring's DMA for the next item stays in flight; red is double-buffered
-        // by item parity so a fast wave's next write cannot race this item's reads)
-        float *rb = red + (it & 1) * NW * EM;
+        // ---- item end: the wave's partial tile goes to reduction slot it % RC; every RC items
+        // (RC = IPW when LDS allows: once, after the stream) the WG sums the slots' NW partials
+        // in a fixed order.  Raw s_barriers: the ring's DMA for later items stays in flight.
         if (ABL & 4) {
-            if (lane < 32 && col < N) d[col] = f2h(cur[0]);
+            if (lane < 16 && col < N) d[col] = f2h(cur[0][0]);
             continue;
         }
+        const int rs = it % RC;
 #pragma unroll
-        for (int r = 0; r < RV; r++) {
-            const int row = acc_row(r, lane);
-            if (row < M) rb[wid * EM + row * 32 + (lane & 31)] = cur[r] * 0.25f;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        for (int e = threadIdx.x; e < EM; e += NW * 64) {
-            float v = 0.f;
+        for (int rg = 0; rg < RG; rg++)
 #pragma unroll
-            for (int w = 0; w < NW; w++) v += rb[w * EM + e];
-            const int row = e >> 5, nn = 32 * t + (e & 31);
-            if (S == 1) {
-                if (nn < N) d[(long)row * N + nn] = f2h(v);
-            } else {
-                __hip_atomic_store(&slabs[((long)z * M + row) * Npad + nn], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int r = 0; r < 4; r++) {
+                const int row = 16 * rg + 4 * (lane >> 4) + r;
+                if (row < M) red[(rs * NW + wid) * EM + row * 16 + (lane & 15)] = cur[rg][r] * 0.25f;
+            }
+        if (rs == RC - 1 || it == nit - 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            for (int e = threadIdx.x; e < (rs + 1) * EM; e += NW * 64) {
+                const int k = e / EM, ee = e - k * EM;
+                float v = 0.f;
+#pragma unroll
+                for (int w = 0; w < NW; w++) v += red[(k * NW + w) * EM + ee];
+                const int row = ee >> 4, nn = 16 * item_tile(it - rs + k) + (ee & 15);
+                if (S == 1) {
+                    if (nn < N) d[(long)row * N + nn] = f2h(v);
+                } else {
+                    __hip_atomic_store(&slabs[((long)z * M + row) * Npad + nn], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (it + 1 < nit) {  // the slots are reused by the next items
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
+    FQ_STAMP(3);
     if (S == 1 || (ABL & 4)) return;
 
-    // ---- split-K fix-up (one item per WG when S > 1): write-through slabs, one ticket per WG,
-    // the last arriver of the tile reduces the S slabs in z order
-    const int t = item_tile(0);
+    // ---- deferred split-K fix-up.  Every item's partial tile went out as write-through (sc1)
+    // slab stores; one drain, then one agent-scope ticket per item (taken in parallel, one lane
+    // each), and the last arriver of a tile sums its S slabs in z order.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(&tickets[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)threadIdx.x < nit) {
+        const int tt = item_tile(threadIdx.x);
+        const uint32_t prev = __hip_atomic_fetch_add(&tickets[tt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = (prev == (uint32_t)(S - 1));
-        if (last) __hip_atomic_store(&tickets[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = last;
+        if (last) __hip_atomic_store(&tickets[tt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[threadIdx.x] = last;
     }
     __syncthreads();
-    if (!*flag) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
-    for (int e = threadIdx.x; e < EM; e += NW * 64) {
-        const int row = e >> 5, nn = 32 * t + (e & 31);
-        float v = 0.f;
-        for (int z0 = 0; z0 < S; z0 += 8) {  // 8 independent loads per round trip
-            float part[8];
+    for (int it = 0; it < nit; it++) {
+        if (!flag[it]) continue;  // workgroup-uniform
+        const int t = item_tile(it);
+        for (int e = threadIdx.x; e < EM; e += NW * 64) {
+            const int row = e >> 4, nn = 16 * t + (e & 15);
+            float v = 0.f;
+            for (int z0 = 0; z0 < S; z0 += 8) {  // 8 independent loads per round trip
+                float part[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                part[u] = (z0 + u < S) ? __hip_atomic_load(&slabs[((long)(z0 + u) * M + row) * Npad + nn],
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0.f;
+                for (int u = 0; u < 8; u++)
+                    part[u] = (z0 + u < S) ? __hip_atomic_load(&slabs[((long)(z0 + u) * M + row) * Npad + nn],
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : 0.f;
 #pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (z0 + u < S) v += part[u];
+                for (int u = 0; u < 8; u++)
+                    if (z0 + u < S) v += part[u];
+            }
+            if (nn < N) d[(long)row * N + nn] = f2h(v);
         }
-        if (nn < N) d[(long)row * N + nn] = f2h(v);
     }
+    FQ_STAMP(4);
 }
 
 // =============================================================================================
 // Prefill kernel (M > 32): MFMA-bound.  Block tile 128 x 128, 4 waves as 2 (M) x 2 (N), each
-// wave 64 x 64 = 2 x 2 tiles of 32x32.  Per 128-wide group the block stages
-//   A: 128 rows x 128 B int8, XOR-swizzled 16-B chunks (chunk ^ ((row>>1)&7)) so the
-//      ds_read_b128 of 16 consecutive rows hits 16 distinct bank slots;
-//   B: 4 n-tiles x 3 KiB packed weights, a straight copy of the fq6 blocks (3 planes x 64 lanes
-//      x 16 B), read back as three conflict-free ds_read_b128 per n-tile and group;
+// wave 64 x 64 = 4 x 4 tiles of 16x16.  Per 128-wide group the block stages
+//   A: 128 rows x 128 B int8, 16-byte chunks XOR-swizzled by (row & 7) (xswz) so each 8-lane
+//      phase of a ds_read_b128 hits 8 distinct bank groups;
+//   B: 8 n-tiles x 1.5 KiB packed weights, a straight copy of the fq6 blocks (3 planes x 64
+//      lanes x 8 B), read back as three ds_read_b64 per n-tile and group;
 //   the 128 x-scales and 128 w-scales of the group,
 // in registers one group ahead (global loads issued before the MFMAs, LDS writes after), with
 // two LDS buffers.  Group accumulators are int32; dequant is fp32 FMA per group.
 // =============================================================================================
 constexpr int PF_BM = 128, PF_BN = 128;
-constexpr int PF_A_BYTES = PF_BM * FQ_GROUP;        // 16 KiB
-constexpr int PF_B_BYTES = (PF_BN / 32) * 3072;  // 12 KiB
+constexpr int PF_A_BYTES = PF_BM * FQ_GROUP;                // 16 KiB
+constexpr int PF_B_BYTES = (PF_BN / 16) * FQ_BLOCK;         // 12 KiB
 constexpr int PF_STAGE = PF_A_BYTES + PF_B_BYTES + 2 * PF_BM * 2 + 2 * PF_BN * 2;  // + xs, ws (x2 spare)
 
 struct PrefillStage {
@@ -341,12 +471,10 @@ struct PrefillStage {
     uint16_t xsv, wsv;
 };
 
-__device__ __forceinline__ int a_lds_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
-
 __device__ __forceinline__ void prefill_gload(PrefillStage &st, const int8_t *__restrict__ xq,
                                               const uint16_t *__restrict__ xs,
                                               const uint32_t *__restrict__ wpk,
-                                              const uint16_t *__restrict__ ws, int M, int N, int K,
+                                              const uint16_t *__restrict__ wsb, int M, int N, int K,
                                               int G, int m0, int t0, int NT, int g, int tid) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -358,10 +486,10 @@ __device__ __forceinline__ void prefill_gload(PrefillStage &st, const int8_t *__
     }
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        const int c = tid + 256 * j;  // 768 chunks of 16 B = 4 n-tiles x 3 KiB
-        const int nt = c / 192, within = c - nt * 192;
+        const int c = tid + 256 * j;  // 768 chunks of 16 B = 8 n-tiles x 1.5 KiB
+        const int nt = c / 96, within = c - nt * 96;
         const int t = t0 + nt;
-        if (t < NT) st.b[j] = reinterpret_cast<const uint4 *>(wpk + (long)(t * G + g) * 768)[within];
+        if (t < NT) st.b[j] = reinterpret_cast<const uint4 *>(wpk + (long)(t * G + g) * (FQ_BLOCK / 4))[within];
         else st.b[j] = make_uint4(0, 0, 0, 0);
     }
     st.xsv = 0;
@@ -370,8 +498,8 @@ __device__ __forceinline__ void prefill_gload(PrefillStage &st, const int8_t *__
         const int m = m0 + tid;
         if (m < M) st.xsv = xs[(long)g * M + m];
     } else {
-        const int n = t0 * 32 + (tid - PF_BM);
-        if (n < N) st.wsv = ws[(long)g * N + n];
+        const int c = tid - PF_BM, t = t0 + c / 16;  // blocked scales, pad columns hold 0
+        if (t < NT) st.wsv = wsb[((long)t * G + g) * 16 + (c & 15)];
     }
 }
 
@@ -379,7 +507,7 @@ __device__ __forceinline__ void prefill_swrite(const PrefillStage &st, char *buf
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int c = tid + 256 * j;
-        *reinterpret_cast<uint4 *>(buf + a_lds_off(c >> 3, c & 7)) = st.a[j];
+        *reinterpret_cast<uint4 *>(buf + (c >> 3) * 128 + xswz(c >> 3, c & 7)) = st.a[j];
     }
     char *bb = buf + PF_A_BYTES;
 #pragma unroll
@@ -390,11 +518,11 @@ __device__ __forceinline__ void prefill_swrite(const PrefillStage &st, char *buf
 
 template <bool DBG>
 __global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
-    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk,
-    const uint16_t *__restrict__ ws, int M, int N, int K, uint16_t *__restrict__ d,
-    int32_t *__restrict__ acc_dbg) {
+    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
+    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
+    const int G = K / FQ_GROUP, NT = (N + 15) / 16;
+    const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
 
@@ -404,78 +532,71 @@ __global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
     const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
     const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
     const int bn = lid % nby, bm = lid / nby;  // N fastest: blocks sharing an A panel are adjacent
-    const int m0 = bm * PF_BM, t0 = bn * (PF_BN / 32);
+    const int m0 = bm * PF_BM, t0 = bn * (PF_BN / 16);
 
-    float out[2][2][16];
+    float out[4][4][4];
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < 4; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int j = 0; j < 4; j++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) out[i][j][r] = 0.f;
+            for (int r = 0; r < 4; r++) out[i][j][r] = 0.f;
 
     PrefillStage st;
-    prefill_gload(st, xq, xs, wpk, ws, M, N, K, G, m0, t0, NT, 0, tid);
+    prefill_gload(st, xq, xs, wpk, wsb, M, N, K, G, m0, t0, NT, 0, tid);
     prefill_swrite(st, smem, tid);
     __syncthreads();
 
     for (int g = 0; g < G; g++) {
         char *buf = smem + (g & 1) * PF_STAGE;
-        if (g + 1 < G) prefill_gload(st, xq, xs, wpk, ws, M, N, K, G, m0, t0, NT, g + 1, tid);
+        if (g + 1 < G) prefill_gload(st, xq, xs, wpk, wsb, M, N, K, G, m0, t0, NT, g + 1, tid);
 
-        v4i bp[2][3];
+        v4i b[4][2];
 #pragma unroll
-        for (int ni = 0; ni < 2; ni++) {
-            const char *bsrc = buf + PF_A_BYTES + (wn * 2 + ni) * 3072 + lane * 16;
-#pragma unroll
-            for (int r = 0; r < 3; r++) bp[ni][r] = *reinterpret_cast<const v4i *>(bsrc + r * 1024);
+        for (int ni = 0; ni < 4; ni++) {
+            const char *bsrc = buf + PF_A_BYTES + (wn * 4 + ni) * FQ_BLOCK + lane * 8;
+            const uint2 q0 = *reinterpret_cast<const uint2 *>(bsrc);
+            const uint2 q1 = *reinterpret_cast<const uint2 *>(bsrc + 512);
+            const uint2 q2 = *reinterpret_cast<const uint2 *>(bsrc + 1024);
+            b[ni][0] = unpack_fq6(q0.x, q1.x, q2.x);
+            b[ni][1] = unpack_fq6(q0.y, q1.y, q2.y);
         }
-        v16i acc[2][2];
+        v4i acc[4][4];
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            v4i a[2], b[2];
+        for (int mi = 0; mi < 4; mi++) {
+            const int row = wm * 64 + mi * 16 + (lane & 15);
+            v4i a[2];
 #pragma unroll
-            for (int mi = 0; mi < 2; mi++) {
-                const int row = wm * 64 + mi * 32 + (lane & 31);
-                a[mi] = *reinterpret_cast<const v4i *>(buf + a_lds_off(row, 2 * s + (lane >> 5)));
+            for (int s = 0; s < 2; s++) a[s] = *reinterpret_cast<const v4i *>(buf + row * 128 + xswz(row, 4 * s + (lane >> 4)));
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++) {
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[0], b[ni][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[1], b[ni][1], acc[mi][ni], 0, 0, 0);
             }
-#pragma unroll
-            for (int ni = 0; ni < 2; ni++) b[ni] = unpack_fq6(bp[ni][0][s], bp[ni][1][s], bp[ni][2][s]);
-#pragma unroll
-            for (int mi = 0; mi < 2; mi++)
-#pragma unroll
-                for (int ni = 0; ni < 2; ni++) {
-                    if (s == 0) acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], v16i{0}, 0, 0, 0);
-                    else acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-                }
         }
 
         const uint16_t *sc = reinterpret_cast<const uint16_t *>(buf + PF_A_BYTES + PF_B_BYTES);
 #pragma unroll
-        for (int ni = 0; ni < 2; ni++) {
-            const int col = wn * 64 + ni * 32 + (lane & 31);
+        for (int ni = 0; ni < 4; ni++) {
+            const int col = wn * 64 + ni * 16 + (lane & 15);
             const __half2 w2 = __half2half2(__ushort_as_half(sc[PF_BM + col]));
 #pragma unroll
-            for (int mi = 0; mi < 2; mi++) {
-                const uint16_t *xr = sc + wm * 64 + mi * 32 + 4 * (lane >> 5);
-#pragma unroll
-                for (int q4 = 0; q4 < 4; q4++) {
-                    const uint2 xv = *reinterpret_cast<const uint2 *>(xr + 8 * q4);
-                    const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&xv.x), w2);
-                    const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&xv.y), w2);
-                    float *o = out[mi][ni] + 4 * q4;
-                    const v16i &c = acc[mi][ni];
-                    o[0] = fmaf((float)c[4 * q4 + 0], __low2float(p01), o[0]);
-                    o[1] = fmaf((float)c[4 * q4 + 1], __high2float(p01), o[1]);
-                    o[2] = fmaf((float)c[4 * q4 + 2], __low2float(p23), o[2]);
-                    o[3] = fmaf((float)c[4 * q4 + 3], __high2float(p23), o[3]);
-                }
+            for (int mi = 0; mi < 4; mi++) {
+                const uint2 xv = *reinterpret_cast<const uint2 *>(sc + wm * 64 + mi * 16 + 4 * (lane >> 4));
+                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&xv.x), w2);
+                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&xv.y), w2);
+                float *o = out[mi][ni];
+                const v4i &c = acc[mi][ni];
+                o[0] = fmaf((float)c[0], __low2float(p01), o[0]);
+                o[1] = fmaf((float)c[1], __high2float(p01), o[1]);
+                o[2] = fmaf((float)c[2], __low2float(p23), o[2]);
+                o[3] = fmaf((float)c[3], __high2float(p23), o[3]);
                 if (DBG) {
-                    const int n = t0 * 32 + col;
+                    const int n = t0 * 16 + col;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        const int m = m0 + wm * 64 + mi * 32 + acc_row(r, lane);
-                        if (m < M && n < N) acc_dbg[((long)m * N + n) * G + g] = acc[mi][ni][r] >> 2;
+                    for (int r = 0; r < 4; r++) {
+                        const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + r;
+                        if (m < M && n < N) acc_dbg[((long)m * N + n) * G + g] = c[r] >> 2;
                     }
                 }
             }
@@ -487,13 +608,13 @@ __global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
     }
 
 #pragma unroll
-    for (int mi = 0; mi < 2; mi++)
+    for (int mi = 0; mi < 4; mi++)
 #pragma unroll
-        for (int ni = 0; ni < 2; ni++) {
-            const int n = t0 * 32 + wn * 64 + ni * 32 + (lane & 31);
+        for (int ni = 0; ni < 4; ni++) {
+            const int n = t0 * 16 + wn * 64 + ni * 16 + (lane & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int m = m0 + wm * 64 + mi * 32 + acc_row(r, lane);
+            for (int r = 0; r < 4; r++) {
+                const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + r;
                 if (m < M && n < N) d[(long)m * N + n] = f2h(out[mi][ni][r] * 0.25f);
             }
         }
@@ -503,12 +624,9 @@ __global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
 // Host side: plan + launch
 // =============================================================================================
 struct DecodePlan {
-    int MT, NW, S, grid, IPW, XS, SS;
+    int MT, S, grid, IPW, RC, XS, SS, xwin;  // xwin: fused fp16 window (0 = not fused)
+    bool fits;
 };
-
-// waves per WG (one WG per CU): 8 for M <= 8, 4 for the larger M > 8 ring slots
-template <int MT> struct DecodeWaves { static constexpr int NW = MT <= 8 ? 8 : 4; };
-static int decode_waves(int MT) { return MT <= 8 ? 8 : 4; }
 static const size_t kLdsMax = 160 * 1024;
 
 static int device_cus() {
@@ -523,50 +641,70 @@ static int device_cus() {
 }
 
 static size_t decode_lds_bytes(const DecodePlan &p, int M, int N, int K) {
+    const int NW = decode_waves(p.MT);
     const int Gz = (K / FQ_GROUP + p.S - 1) / p.S;
-    const int ngmax = (Gz + p.NW - 1) / p.NW;
-    return (size_t)p.NW * decode_wave_lds(p.MT, p.XS, p.SS, ngmax, ngmax * p.IPW, M, (N & 1) == 0) +
-           (size_t)2 * p.NW * M * 32 * 4 + 16;
+    const int ngmax = (Gz + NW - 1) / NW;
+    return (size_t)NW * decode_wave_lds(p.MT, p.XS, p.SS, ngmax, ngmax * p.IPW, M, p.xwin) +
+           (size_t)p.RC * NW * M * 16 * 4 + 4 * (size_t)p.IPW + 16;
 }
 
-static DecodePlan decode_plan(int M, int N, int K) {
+// fused: only the fully staged variant (the quantizer writes straight into the staged regions);
+// `fits` is false when that does not fit LDS and the caller must quantize separately.
+static DecodePlan decode_plan(int M, int N, int K, bool fused) {
     DecodePlan p;
     p.MT = M <= 4 ? 4 : (M <= 8 ? 8 : (M <= 16 ? 16 : 32));
-    p.NW = decode_waves(p.MT);
-    const int NT = (N + 31) / 32, G = K / FQ_GROUP;
+    const int NT = (N + 15) / 16, G = K / FQ_GROUP;
     const int cus = device_cus();
-    // Few tiles: split K so that ~one item per CU streams (never below one group per wave).
-    // Many tiles: whole tiles, WGs persistent over them (items w, w + grid, ...).
-    int S = 1;
-    if (NT < cus) {
-        S = cus / NT;
-        int cap = G / p.NW;
-        if (cap < 1) cap = 1;
-        if (S > cap) S = cap;
-        if (S < 1) S = 1;
+    const int NW = decode_waves(p.MT);
+    // k-split S: minimise the largest per-wave block count (items per WG x groups per wave),
+    // +3 for the fix-up of S > 1 (measured 1.1-1.7 us, tools/stamps.py: ~3 blocks per wave at
+    // the whole-chip streaming rate).  S divides the grid so that z = blockIdx % S is fixed per
+    // WG; ties keep the smaller S.
+    long best = -1;
+    p.S = 1;
+    for (int S = 1; S <= G && S <= cus; S++) {
+        const int items = NT * S;
+        const int grid = items < cus ? items : cus;
+        if (grid % S) continue;
+        const long ipw = (items + grid - 1) / grid;
+        const long gz = (G + S - 1) / S;
+        const long cost = ipw * ((gz + NW - 1) / NW) + (S > 1 ? 3 : 0);
+        if (best < 0 || cost < best) {
+            best = cost;
+            p.S = S;
+        }
     }
-    p.S = S;
-    const int items = NT * S;
+    const int items = NT * p.S;
     p.grid = items < cus ? items : cus;
     p.IPW = (items + p.grid - 1) / p.grid;
-    // staging choice: the most staged variant that fits LDS
+    // staging: the most staged variant that fits LDS, then as many reduction slots as fit
+    // (RC = IPW: one reduction after the whole stream)
+    // (fused: the fully staged variant with the largest fp16 window that fits)
     const int modes[3][2] = {{0, 0}, {1, 0}, {1, 1}};
-    for (int m = (p.MT <= 4 ? 0 : 1); m < 3; m++) {
+    const int nm = fused ? 1 : 3;
+    p.fits = false;
+    for (int m = 0; m < nm && !p.fits; m++) {
         p.XS = modes[m][0];
         p.SS = modes[m][1];
-        if (decode_lds_bytes(p, M, N, K) <= kLdsMax) break;
+        for (p.xwin = fused ? 32 : 0; !p.fits && p.xwin >= (fused ? 4 : 0); p.xwin = p.xwin ? p.xwin / 2 : -1) {
+            for (p.RC = p.IPW; p.RC >= 1 && !p.fits; p.RC--) p.fits = decode_lds_bytes(p, M, N, K) <= kLdsMax;
+            if (p.fits) {
+                p.RC++;
+                break;
+            }
+        }
     }
     return p;
 }
 
-static const size_t kTicketBytes = 256 * 1024;  // tickets for up to 65536 n-tiles
+static const size_t kTicketBytes = 256 * 1024;  // tickets for up to 65536 16-column tiles
 
 extern "C" size_t fq_gemm_workspace_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
     if (M > 32) return 0;
-    DecodePlan p = decode_plan(M, N, K);
+    DecodePlan p = decode_plan(M, N, K, false);  // S does not depend on the staging variant
     if (p.S == 1) return 0;
-    const size_t Npad = (size_t)((N + 31) / 32) * 32;
+    const size_t Npad = (size_t)((N + 15) / 16) * 16;
     return kTicketBytes + (size_t)p.S * M * Npad * sizeof(float);
 }
 
@@ -580,90 +718,120 @@ extern "C" fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_
 
 #ifdef FQ_DEV_ABLATION
 #include <cstdlib>
+extern "C" int fq_dev_stamps(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fq_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
 static int dev_ablation() {
     const char *e = getenv("FQ_DEV_ABLATION");
     return e ? atoi(e) : 0;
 }
 #endif
 
-template <int MT, int XS, int SS, bool DBG>
-static fq_status launch_decode(const DecodePlan &p, const int8_t *xq, const uint16_t *xs,
-                               const void *wpk, const uint16_t *ws, int M, int N, int K, uint16_t *d,
-                               int32_t *acc_dbg, void *workspace, hipStream_t stream) {
-    constexpr int NW = DecodeWaves<MT>::NW;
-    uint32_t *tickets = p.S > 1 ? (uint32_t *)workspace : nullptr;
-    float *slabs = p.S > 1 ? (float *)((char *)workspace + kTicketBytes) : nullptr;
-    const size_t lds = decode_lds_bytes(p, M, N, K);
+struct DecodeArgs {
+    const int8_t *xq;
+    const uint16_t *xs, *xh;
+    int abits;
+    const void *wpk;
+    int M, N, K;
+    uint16_t *d;
+    int32_t *acc_dbg;
+    void *workspace;
+};
+
+template <int MT, int XS, int SS, bool FUSE, bool DBG>
+static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
+    uint32_t *tickets = p.S > 1 ? (uint32_t *)a.workspace : nullptr;
+    float *slabs = p.S > 1 ? (float *)((char *)a.workspace + kTicketBytes) : nullptr;
+    const size_t lds = decode_lds_bytes(p, a.M, a.N, a.K);
+    const dim3 grid(p.grid), block(decode_waves(MT) * 64);
 #ifdef FQ_DEV_ABLATION
-    if (!DBG && MT == 4 && XS == 0 && SS == 0) {
+    if (!DBG && MT == 4 && XS == 0 && SS == 0) {  // (the fused and the unfused kernel)
         const int abl = dev_ablation();
-#define FQ_ABL(v)                                                                                          \
-    if (abl == v) {                                                                                          \
-        hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, NW, XS, SS, DBG, v>), dim3(p.grid), dim3(NW * 64), lds,  \
-                           stream, xq, xs, (const uint32_t *)wpk, ws, M, N, K, d, acc_dbg, slabs, tickets,    \
-                           p.S, p.IPW);                                                                      \
-        FQ_LAUNCH_CHECK();                                                                                   \
-        return FQ_OK;                                                                                        \
+#define FQ_ABL(v)                                                                                           \
+    if (abl == v) {                                                                                           \
+        hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
+                           a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
+                           slabs, tickets, p.S, p.IPW, p.RC, p.xwin);                                         \
+        FQ_LAUNCH_CHECK();                                                                                    \
+        return FQ_OK;                                                                                         \
     }
-        FQ_ABL(2) FQ_ABL(4) FQ_ABL(6) FQ_ABL(8) FQ_ABL(14)
+        FQ_ABL(2) FQ_ABL(4) FQ_ABL(6) FQ_ABL(8) FQ_ABL(14) FQ_ABL(16)
 #undef FQ_ABL
     }
 #endif
-    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, NW, XS, SS, DBG>), dim3(p.grid), dim3(NW * 64), lds, stream,
-                       xq, xs, (const uint32_t *)wpk, ws, M, N, K, d, acc_dbg, slabs, tickets, p.S, p.IPW);
+    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG>), grid, block, lds, stream, a.xq, a.xs, a.xh,
+                       a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S, p.IPW,
+                       p.RC, p.xwin);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
 
-template <int MT, bool DBG>
-static fq_status dispatch_modes(const DecodePlan &p, const int8_t *xq, const uint16_t *xs, const void *wpk,
-                                const uint16_t *ws, int M, int N, int K, uint16_t *d, int32_t *acc_dbg,
-                                void *workspace, hipStream_t stream) {
-    if (MT <= 4 && p.XS == 0) return launch_decode<MT, 0, 0, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
-    if (p.SS == 0) return launch_decode<MT, 1, 0, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
-    return launch_decode<MT, 1, 1, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
+template <int MT, bool FUSE, bool DBG>
+static fq_status dispatch_modes(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
+    if (FUSE) return launch_decode<MT, 0, 0, true, DBG>(p, a, stream);
+    if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG>(p, a, stream);
+    if (p.SS == 0) return launch_decode<MT, 1, 0, false, DBG>(p, a, stream);
+    return launch_decode<MT, 1, 1, false, DBG>(p, a, stream);
 }
 
-template <bool DBG>
-static fq_status dispatch_decode(const DecodePlan &p, const int8_t *xq, const uint16_t *xs,
-                                 const void *wpk, const uint16_t *ws, int M, int N, int K, uint16_t *d,
-                                 int32_t *acc_dbg, void *workspace, hipStream_t stream) {
-    if (decode_lds_bytes(p, M, N, K) > kLdsMax) return FQ_ERR_SHAPE;  // cannot happen for K <= 2^20
+template <bool FUSE, bool DBG>
+static fq_status dispatch_decode(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
+    if (!p.fits) return FQ_ERR_SHAPE;  // the unfused plan always fits for K <= 2^20
     switch (p.MT) {
-        case 4: return dispatch_modes<4, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
-        case 8: return dispatch_modes<8, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
-        case 16: return dispatch_modes<16, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
-        default: return dispatch_modes<32, DBG>(p, xq, xs, wpk, ws, M, N, K, d, acc_dbg, workspace, stream);
+        case 4: return dispatch_modes<4, FUSE, DBG>(p, a, stream);
+        case 8: return dispatch_modes<8, FUSE, DBG>(p, a, stream);
+        case 16: return dispatch_modes<16, FUSE, DBG>(p, a, stream);
+        default: return dispatch_modes<32, FUSE, DBG>(p, a, stream);
     }
 }
 
-extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const void *w_packed,
-                                  const uint16_t *ws, int M, int N, int K, int abits, uint16_t *d,
-                                  int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
-                                  fq_stream_t stream) {
-    if (!xq || !xs || !w_packed || !ws || !d) return FQ_ERR_NULL;
+extern "C" size_t fq_linear_act_scratch_bytes(int M, int N, int K) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
+    if (M <= 32 && decode_plan(M, N, K, true).fits) return 0;
+    return (size_t)M * K + (size_t)M * (K / FQ_GROUP) * 2;
+}
+
+// One-launch decode linear (quantize + GEMM) when the staged plan fits; FQ_ERR_SHAPE otherwise.
+fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
+                                 uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
+                                 hipStream_t s, bool *launched) {
+    *launched = false;
+    if (M > 32) return FQ_OK;
+    DecodePlan p = decode_plan(M, N, K, true);
+    if (!p.fits) return FQ_OK;
+    const size_t need = fq_gemm_workspace_bytes(M, N, K);
+    if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
+    DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace};
+    *launched = true;
+    return acc_dbg ? dispatch_decode<true, true>(p, a, s) : dispatch_decode<true, false>(p, a, s);
+}
+
+extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N,
+                                  int K, int abits, uint16_t *d, int32_t *acc_dbg, void *workspace,
+                                  size_t workspace_bytes, fq_stream_t stream) {
+    if (!xq || !xs || !w_packed || !d) return FQ_ERR_NULL;
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
-    if ((size_t)((N + 31) / 32) > kTicketBytes / 4) return FQ_ERR_SHAPE;
+    if ((size_t)((N + 15) / 16) > kTicketBytes / 4) return FQ_ERR_SHAPE;
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     // The kernels are bit-width agnostic (int8 activations, values bounded by abits); abits is
     // validated for API parity with FLEXQGEMMWrapper(X_BITS, W_BITS, SIGNED).
     hipStream_t s = (hipStream_t)stream;
     if (M <= 32) {
-        DecodePlan p = decode_plan(M, N, K);
+        DecodePlan p = decode_plan(M, N, K, false);
         const size_t need = fq_gemm_workspace_bytes(M, N, K);
         if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
-        return acc_dbg ? dispatch_decode<true>(p, xq, xs, w_packed, ws, M, N, K, d, acc_dbg, workspace, s)
-                       : dispatch_decode<false>(p, xq, xs, w_packed, ws, M, N, K, d, acc_dbg, workspace, s);
+        DecodeArgs a = {xq, xs, nullptr, abits, w_packed, M, N, K, d, acc_dbg, workspace};
+        return acc_dbg ? dispatch_decode<false, true>(p, a, s) : dispatch_decode<false, false>(p, a, s);
     }
-    const int NT = (N + 31) / 32;
-    dim3 grid((M + PF_BM - 1) / PF_BM, (NT + 3) / 4);
+    const int NT = (N + 15) / 16;
+    dim3 grid((M + PF_BM - 1) / PF_BM, (NT + PF_BN / 16 - 1) / (PF_BN / 16));
     const size_t lds = 2 * (size_t)PF_STAGE;
     if (acc_dbg)
         hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, grid, dim3(256), lds, s, xq, xs,
-                           (const uint32_t *)w_packed, ws, M, N, K, d, acc_dbg);
+                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
     else
         hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, grid, dim3(256), lds, s, xq, xs,
-                           (const uint32_t *)w_packed, ws, M, N, K, d, acc_dbg);
+                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }

@@ -24,42 +24,18 @@ __global__ __launch_bounds__(256) void fq_quantize_act_kernel(
     const int sub = lane & 15;  // position inside the group
     const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-    const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
-    const float fhi = (float)hi;
 
     for (long chunk = wave; chunk * 4 < T; chunk += nwaves) {
         const long gi = chunk * 4 + (lane >> 4);  // flat group index of this lane
         const bool valid = gi < T;
         uint4 raw = make_uint4(0, 0, 0, 0);
         if (valid) raw = *reinterpret_cast<const uint4 *>(x + gi * FQ_GROUP + sub * 8);
-        uint16_t h[8] = {(uint16_t)raw.x, (uint16_t)(raw.x >> 16), (uint16_t)raw.y,
-                         (uint16_t)(raw.y >> 16), (uint16_t)raw.z, (uint16_t)(raw.z >> 16),
-                         (uint16_t)raw.w, (uint16_t)(raw.w >> 16)};
-        float v[8];
-        float mx = -1.0f;  // the reference seeds the fp16 max with -1 (bit_packing.cu:139)
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            v[i] = h2f(h[i]);
-            mx = fmaxf(mx, fabsf(v[i]));  // fmaxf drops a NaN operand, like __hmax
-        }
-        // max over the 16 lanes of the group (xor 8,4,2,1 stays inside a 16-lane DPP row)
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        const float maxv = mx / fhi;  // IEEE fp32 division (no fast-math in this build)
-        const uint16_t sh = f2h(maxv);
-        const float r = h2f(sh);
-        int q[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) q[i] = sat_clamp(round_half_away(v[i] / r), lo, hi);
-
+        uint2 codes;
+        const uint16_t sh = quant_group16(raw, bits, codes);
         const long m = gi / G, g = gi - (gi / G) * G;
         if (MODE == 0) {
             if (valid) {
-                uint32_t w0 = (q[0] & 255) | ((q[1] & 255) << 8) | ((q[2] & 255) << 16) |
-                              ((uint32_t)(q[3] & 255) << 24);
-                uint32_t w1 = (q[4] & 255) | ((q[5] & 255) << 8) | ((q[6] & 255) << 16) |
-                              ((uint32_t)(q[7] & 255) << 24);
-                *reinterpret_cast<uint2 *>(xq + gi * FQ_GROUP + sub * 8) = make_uint2(w0, w1);
+                *reinterpret_cast<uint2 *>(xq + gi * FQ_GROUP + sub * 8) = codes;
                 if (sub == 0) xs[g * M + m] = sh;
             }
         } else {
@@ -70,7 +46,7 @@ __global__ __launch_bounds__(256) void fq_quantize_act_kernel(
             for (int b = 0; b < bits; b++) {
                 uint32_t byte = 0;
 #pragma unroll
-                for (int i = 0; i < 8; i++) byte |= (uint32_t)((q[i] >> b) & 1) << (7 - i);
+                for (int i = 0; i < 8; i++) byte |= (((i < 4 ? codes.x : codes.y) >> (8 * (i & 3) + b)) & 1u) << (7 - i);
                 uint32_t word = byte << (8 * (3 - u));
                 word |= __shfl_xor(word, 1, 64);
                 word |= __shfl_xor(word, 2, 64);
@@ -161,11 +137,15 @@ extern "C" fq_status fq_ref_bit_packing(const int32_t *in, int32_t *packed, int 
 
 // =============================================================================================
 // fq6 weight layout (oracle fqo_pack_fq6):
-//   uint32 [Npad/32][K/128][3 plane r][64 lane][4 kstep s]
-//   lane l, kstep s: column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j (j = 0..15)
+//   uint32 [Npad/16][K/128][3 plane r][64 lane][2 kstep s]
+//   lane l, kstep s: column n = 16t + (l&15), k = 128g + 64s + 16(l>>4) + j (j = 0..15),
+//   i.e. the B operand of v_mfma_i32_16x16x64_i8 for k-step s of the group
 //   byte b of word (r, s) = ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3)
-// One thread builds one lane's 48 bytes of a (tile, group) block and writes its three 16-byte
-// plane words, so each wave writes three 1 KiB contiguous runs.
+// One thread builds one lane's 24 bytes of a (tile, group) block and writes its three 8-byte
+// plane words, so each wave writes three 512 B contiguous runs.  The image ends with the group
+// scales blocked the same way, fp16 [Npad/16][K/128][16] (lanes 0..15 write them): a wave's
+// scales for consecutive groups of one tile are contiguous, so the GEMM stages them with a few
+// coalesced DMAs and each scale line is fetched by exactly one CU.
 // =============================================================================================
 __device__ __forceinline__ uint32_t fq6_word(const int v[16], int r) {
     uint32_t w = 0;
@@ -184,29 +164,43 @@ __device__ __forceinline__ void fq6_lane(long slot, int G, int &t, int &g, int &
     g = (int)(tg % G);
     t = (int)(tg / G);
 }
+__device__ __forceinline__ int fq6_col(int t, int l) { return 16 * t + (l & 15); }
+__device__ __forceinline__ int fq6_k(int g, int s, int l) { return 128 * g + 64 * s + 16 * (l >> 4); }
 
-__device__ __forceinline__ void fq6_store(uint32_t *__restrict__ out, long slot, int l, const uint32_t p[3][4]) {
-    const long base = (slot >> 6) * 768 + l * 4;  // ((t*G+g)*3 + r)*256 + l*4
+__device__ __forceinline__ void fq6_store(uint32_t *__restrict__ out, long slot, int l, const uint32_t p[3][2]) {
+    const long base = (slot >> 6) * 384 + l * 2;  // ((t*G+g)*3 + r)*128 + l*2
 #pragma unroll
-    for (int r = 0; r < 3; r++)
-        *reinterpret_cast<uint4 *>(out + base + r * 256) = make_uint4(p[r][0], p[r][1], p[r][2], p[r][3]);
+    for (int r = 0; r < 3; r++) *reinterpret_cast<uint2 *>(out + base + r * 128) = make_uint2(p[r][0], p[r][1]);
 }
 
-__global__ void fq_pack_w6_kernel(const int8_t *__restrict__ wq, int N, int K,
-                                  uint32_t *__restrict__ out) {
-    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 64;
+__host__ __device__ static inline long fq6_slots(int N, int K) { return (long)((N + 15) / 16) * (K / FQ_GROUP) * 64; }
+// the blocked scale region of an image: fp16 [Npad/16][G][16] after the weight blocks
+__device__ __forceinline__ uint16_t *fq6_scales(uint32_t *img, int N, int K) {
+    return reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(img) + (size_t)((N + 15) / 16) * (K / FQ_GROUP) * 1536);
+}
+__device__ __forceinline__ const uint16_t *fq6_scales(const uint32_t *img, int N, int K) {
+    return reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(img) + (size_t)((N + 15) / 16) * (K / FQ_GROUP) * 1536);
+}
+// lanes 0..15 of a (t, g) slot store the 16 scales of the block (0 for pad columns)
+__device__ __forceinline__ void fq6_store_scale(uint32_t *img, int N, int K, long slot, int l, int n, uint16_t v) {
+    if (l < 16) fq6_scales(img, N, K)[(slot >> 6) * 16 + l] = (n < N) ? v : (uint16_t)0;
+}
+
+__global__ void fq_pack_w6_kernel(const int8_t *__restrict__ wq, const uint16_t *__restrict__ ws, int N,
+                                  int K, uint32_t *__restrict__ out) {
+    const int G = K / FQ_GROUP;
+    const long total = fq6_slots(N, K);
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
         int t, g, l;
         fq6_lane(slot, G, t, g, l);
-        const int n = 32 * t + (l & 31);
-        uint32_t p[3][4];
+        const int n = fq6_col(t, l);
+        uint32_t p[3][2];
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
+        for (int s = 0; s < 2; s++) {
             int v[16];
             if (n < N) {
-                const int4 raw = *reinterpret_cast<const int4 *>(wq + (long)n * K + 128 * g + 32 * s + 16 * (l >> 5));
+                const int4 raw = *reinterpret_cast<const int4 *>(wq + (long)n * K + fq6_k(g, s, l));
                 const int w[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
                 for (int j = 0; j < 16; j++) v[j] = (int)(int8_t)((w[j >> 2] >> (8 * (j & 3))) & 255);
@@ -218,27 +212,28 @@ __global__ void fq_pack_w6_kernel(const int8_t *__restrict__ wq, int N, int K,
             for (int r = 0; r < 3; r++) p[r][s] = fq6_word(v, r);
         }
         fq6_store(out, slot, l, p);
+        fq6_store_scale(out, N, K, slot, l, n, n < N ? ws[(long)g * N + n] : 0);
     }
 }
 
 __global__ void fq_unpack_w6_kernel(const uint32_t *__restrict__ in, int N, int K,
-                                    int8_t *__restrict__ wq) {
-    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 64;
+                                    int8_t *__restrict__ wq, uint16_t *__restrict__ ws) {
+    const int G = K / FQ_GROUP;
+    const long total = fq6_slots(N, K);
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
         int t, g, l;
         fq6_lane(slot, G, t, g, l);
-        const int n = 32 * t + (l & 31);
+        const int n = fq6_col(t, l);
         if (n >= N) continue;
-        const long base = (slot >> 6) * 768 + l * 4;
-        const uint4 P0 = *reinterpret_cast<const uint4 *>(in + base);
-        const uint4 P1 = *reinterpret_cast<const uint4 *>(in + base + 256);
-        const uint4 P2 = *reinterpret_cast<const uint4 *>(in + base + 512);
-        const uint32_t q0[4] = {P0.x, P0.y, P0.z, P0.w}, q1[4] = {P1.x, P1.y, P1.z, P1.w},
-                       q2[4] = {P2.x, P2.y, P2.z, P2.w};
+        if (ws && l < 16) ws[(long)g * N + n] = fq6_scales(in, N, K)[(slot >> 6) * 16 + l];
+        const long base = (slot >> 6) * 384 + l * 2;
+        const uint2 P0 = *reinterpret_cast<const uint2 *>(in + base);
+        const uint2 P1 = *reinterpret_cast<const uint2 *>(in + base + 128);
+        const uint2 P2 = *reinterpret_cast<const uint2 *>(in + base + 256);
+        const uint32_t q0[2] = {P0.x, P0.y}, q1[2] = {P1.x, P1.y}, q2[2] = {P2.x, P2.y};
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
+        for (int s = 0; s < 2; s++) {
             v4i o = unpack_fq6(q0[s], q1[s], q2[s]);
             int4 res;
             int *rp = reinterpret_cast<int *>(&res);
@@ -252,7 +247,7 @@ __global__ void fq_unpack_w6_kernel(const uint32_t *__restrict__ in, int N, int 
                 }
                 rp[d] = (int)y;
             }
-            *reinterpret_cast<int4 *>(wq + (long)n * K + 128 * g + 32 * s + 16 * (l >> 5)) = res;
+            *reinterpret_cast<int4 *>(wq + (long)n * K + fq6_k(g, s, l)) = res;
         }
     }
 }
@@ -265,25 +260,27 @@ static int grid_for(long total) {
 
 extern "C" size_t fq_packed_w_bytes(int N, int K) {
     if (N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
-    return (size_t)((N + 31) / 32) * (K / FQ_GROUP) * 3072;
+    return (size_t)((N + 15) / 16) * (K / FQ_GROUP) * (1536 + 32);
 }
 
-extern "C" fq_status fq_pack_w6(const int8_t *wq, int N, int K, void *w_packed, fq_stream_t stream) {
-    if (!wq || !w_packed) return FQ_ERR_NULL;
+extern "C" fq_status fq_pack_w6(const int8_t *wq, const uint16_t *ws, int N, int K, void *w_packed,
+                                fq_stream_t stream) {
+    if (!wq || !ws || !w_packed) return FQ_ERR_NULL;
     if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
+    const long total = fq6_slots(N, K);
     hipLaunchKernelGGL(fq_pack_w6_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
-                       wq, N, K, (uint32_t *)w_packed);
+                       wq, ws, N, K, (uint32_t *)w_packed);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
 
-extern "C" fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, fq_stream_t stream) {
+extern "C" fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, uint16_t *ws,
+                                  fq_stream_t stream) {
     if (!wq || !w_packed) return FQ_ERR_NULL;
     if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
+    const long total = fq6_slots(N, K);
     hipLaunchKernelGGL(fq_unpack_w6_kernel, dim3(grid_for(total)), dim3(256), 0,
-                       (hipStream_t)stream, (const uint32_t *)w_packed, N, K, wq);
+                       (hipStream_t)stream, (const uint32_t *)w_packed, N, K, wq, ws);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
@@ -318,18 +315,18 @@ __global__ void fq_weight_scale_kernel(const uint16_t *__restrict__ w, int N, in
 __global__ void fq_weight_pack_kernel(const uint16_t *__restrict__ w, const uint16_t *__restrict__ ws,
                                       int N, int K, uint32_t *__restrict__ out,
                                       int8_t *__restrict__ wq_out) {
-    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 64;
+    const int G = K / FQ_GROUP;
+    const long total = fq6_slots(N, K);
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
         int t, g, l;
         fq6_lane(slot, G, t, g, l);
-        const int n = 32 * t + (l & 31);
-        uint32_t p[3][4];
+        const int n = fq6_col(t, l);
+        uint32_t p[3][2];
         const float r = (n < N) ? h2f(ws[(long)g * N + n]) : 1.0f;
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const int k0 = 128 * g + 32 * s + 16 * (l >> 5);
+        for (int s = 0; s < 2; s++) {
+            const int k0 = fq6_k(g, s, l);
             int v[16];
             if (n < N) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(w + (long)n * K + k0);
@@ -354,6 +351,7 @@ __global__ void fq_weight_pack_kernel(const uint16_t *__restrict__ w, const uint
             for (int rr = 0; rr < 3; rr++) p[rr][s] = fq6_word(v, rr);
         }
         fq6_store(out, slot, l, p);
+        fq6_store_scale(out, N, K, slot, l, n, n < N ? ws[(long)g * N + n] : 0);
     }
 }
 
@@ -364,7 +362,7 @@ extern "C" fq_status fq_quantize_pack_w6(const uint16_t *w, int N, int K, void *
     hipLaunchKernelGGL(fq_weight_scale_kernel, dim3(quant_grid((long)N * (K / FQ_GROUP))), dim3(256),
                        0, (hipStream_t)stream, w, N, K, ws);
     FQ_LAUNCH_CHECK();
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
+    const long total = fq6_slots(N, K);
     hipLaunchKernelGGL(fq_weight_pack_kernel, dim3(grid_for(total)), dim3(256), 0,
                        (hipStream_t)stream, w, ws, N, K, (uint32_t *)w_packed, wq_out);
     FQ_LAUNCH_CHECK();
@@ -386,26 +384,27 @@ __device__ __forceinline__ int bitplane_value(const int32_t *__restrict__ planes
     return v;
 }
 
-__global__ void fq_import_ref_w_kernel(const int32_t *__restrict__ planes, int N, int K,
-                                       uint32_t *__restrict__ out) {
-    const int G = K / FQ_GROUP, NT = (N + 31) / 32;
-    const long total = (long)NT * G * 64;
+__global__ void fq_import_ref_w_kernel(const int32_t *__restrict__ planes, const uint16_t *__restrict__ ws,
+                                       int N, int K, uint32_t *__restrict__ out) {
+    const int G = K / FQ_GROUP;
+    const long total = fq6_slots(N, K);
     for (long slot = (long)blockIdx.x * blockDim.x + threadIdx.x; slot < total;
          slot += (long)gridDim.x * blockDim.x) {
         int t, g, l;
         fq6_lane(slot, G, t, g, l);
-        const int n = 32 * t + (l & 31);
-        uint32_t p[3][4];
+        const int n = fq6_col(t, l);
+        uint32_t p[3][2];
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
+        for (int s = 0; s < 2; s++) {
             int v[16];
-            const int k0 = 128 * g + 32 * s + 16 * (l >> 5);
+            const int k0 = fq6_k(g, s, l);
 #pragma unroll
             for (int j = 0; j < 16; j++) v[j] = (n < N) ? bitplane_value(planes, N, 6, n, k0 + j) : 0;
 #pragma unroll
             for (int r = 0; r < 3; r++) p[r][s] = fq6_word(v, r);
         }
         fq6_store(out, slot, l, p);
+        fq6_store_scale(out, N, K, slot, l, n, n < N ? ws[(long)g * N + n] : 0);
     }
 }
 
@@ -422,13 +421,13 @@ __global__ void fq_import_ref_x_kernel(const int32_t *__restrict__ planes,
     }
 }
 
-extern "C" fq_status fq_import_ref_w(const int32_t *w_bitplanes, int N, int K, void *w_packed,
-                                     fq_stream_t stream) {
-    if (!w_bitplanes || !w_packed) return FQ_ERR_NULL;
+extern "C" fq_status fq_import_ref_w(const int32_t *w_bitplanes, const uint16_t *w_scale, int N, int K,
+                                     void *w_packed, fq_stream_t stream) {
+    if (!w_bitplanes || !w_scale || !w_packed) return FQ_ERR_NULL;
     if (N <= 0 || K <= 0 || K % FQ_GROUP || (N > 8 && N % 8)) return FQ_ERR_SHAPE;
-    const long total = (long)((N + 31) / 32) * (K / FQ_GROUP) * 64;
+    const long total = fq6_slots(N, K);
     hipLaunchKernelGGL(fq_import_ref_w_kernel, dim3(grid_for(total)), dim3(256), 0,
-                       (hipStream_t)stream, w_bitplanes, N, K, (uint32_t *)w_packed);
+                       (hipStream_t)stream, w_bitplanes, w_scale, N, K, (uint32_t *)w_packed);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }

@@ -68,27 +68,40 @@ def workspace(device, nbytes, stream_handle):
 
 # ------------------------------------------------------------------------- weights
 
-def pack_w6(wq):
-    """int8 codes [N,K] in [-32,31] -> fq6 packed uint8 tensor."""
+def _ws_ok(ws, N, K, dev):
+    _dev(ws, torch.float16, "ws", 2)
+    _need(tuple(ws.shape) == (K // GROUP, N), f"ws must be [K/128, N] = {(K // GROUP, N)}")
+    _need(ws.device == dev, "ws must be on the weights' device")
+
+
+def pack_w6(wq, ws):
+    """int8 codes [N,K] in [-32,31] + fp16 group scales [K/128, N] -> weight image (uint8)."""
     _dev(wq, torch.int8, "wq", 2)
     N, K = wq.shape
     _k_ok(K)
+    _ws_ok(ws, N, K, wq.device)
     out = torch.empty(packed_w_bytes(N, K), dtype=torch.uint8, device=wq.device)
-    _lib.call("fq_pack_w6", _ptr(wq), N, K, _ptr(out), _stream(wq))
+    _lib.call("fq_pack_w6", _ptr(wq), _ptr(ws), N, K, _ptr(out), _stream(wq))
     return out
 
 
 def unpack_w6(wpk, N, K):
+    """Weight image -> (int8 codes [N,K], fp16 scales [K/128, N])."""
+    _img_ok(wpk, N, K)
+    out = torch.empty((N, K), dtype=torch.int8, device=wpk.device)
+    ws = torch.empty((K // GROUP, N), dtype=torch.float16, device=wpk.device)
+    _lib.call("fq_unpack_w6", _ptr(wpk), N, K, _ptr(out), _ptr(ws), _stream(wpk))
+    return out, ws
+
+
+def _img_ok(wpk, N, K):
     _dev(wpk, torch.uint8, "w_packed", 1)
     _k_ok(K)
-    _need(wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
-    out = torch.empty((N, K), dtype=torch.int8, device=wpk.device)
-    _lib.call("fq_unpack_w6", _ptr(wpk), N, K, _ptr(out), _stream(wpk))
-    return out
+    _need(N > 0 and wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
 
 
 def quantize_pack_w6(w, return_codes=False):
-    """fp16 weight [N,K] -> (fq6 packed, ws fp16 [K/128, N]) (+ int8 codes if requested)."""
+    """fp16 weight [N,K] -> (weight image, ws fp16 [K/128, N]) (+ int8 codes if requested)."""
     _dev(w, torch.float16, "w", 2)
     N, K = w.shape
     _k_ok(K)
@@ -115,7 +128,7 @@ def quantize_act(x, abits):
 
 # ------------------------------------------------------------------------- GEMM
 
-def gemm_w6ax(xq, xs, wpk, ws, N, abits=6, return_acc=False, out=None):
+def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None):
     """d fp16 [M,N] from quantized operands; with return_acc also the int32 group accumulators
     [M, N, K/128] (bit-exact debug output)."""
     _dev(xq, torch.int8, "xq", 2)
@@ -123,13 +136,10 @@ def gemm_w6ax(xq, xs, wpk, ws, N, abits=6, return_acc=False, out=None):
     _k_ok(K)
     _dev(xs, torch.float16, "xs", 2)
     _need(tuple(xs.shape) == (K // GROUP, M), f"xs must be [K/128, M] = {(K // GROUP, M)}")
-    _dev(wpk, torch.uint8, "w_packed", 1)
-    _need(wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
-    _dev(ws, torch.float16, "ws", 2)
-    _need(tuple(ws.shape) == (K // GROUP, N), f"ws must be [K/128, N] = {(K // GROUP, N)}")
+    _img_ok(wpk, N, K)
     _need(abits in (6, 8), "abits must be 6 or 8")
     dev = xq.device
-    for t in (xs, wpk, ws):
+    for t in (xs, wpk):
         _need(t.device == dev, "all operands must be on one device")
     if out is None:
         out = torch.empty((M, N), dtype=torch.float16, device=dev)
@@ -140,32 +150,40 @@ def gemm_w6ax(xq, xs, wpk, ws, N, abits=6, return_acc=False, out=None):
     s = _stream(xq)
     nb = gemm_workspace_bytes(M, N, K)
     wbuf = workspace(dev, nb, s.value)
-    _lib.call("fq_gemm_w6ax", _ptr(xq), _ptr(xs), _ptr(wpk), _ptr(ws), M, N, K, abits, _ptr(out),
+    _lib.call("fq_gemm_w6ax", _ptr(xq), _ptr(xs), _ptr(wpk), M, N, K, abits, _ptr(out),
               _ptr(acc), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
     return (out, acc) if return_acc else out
 
 
-def linear_w6ax(x, wpk, ws, N, abits=6, out=None):
+def linear_w6ax(x, wpk, N, abits=6, out=None):
     """Quantize + GEMM (FLEXQGEMMWrapper::gemm(const half* A ...)) for fp16 x [M,K]."""
     _dev(x, torch.float16, "x", 2)
     M, K = x.shape
     _k_ok(K)
-    _dev(wpk, torch.uint8, "w_packed", 1)
-    _need(wpk.numel() == packed_w_bytes(N, K), "w_packed size does not match (N, K)")
-    _dev(ws, torch.float16, "ws", 2)
-    _need(tuple(ws.shape) == (K // GROUP, N), f"ws must be [K/128, N] = {(K // GROUP, N)}")
+    _img_ok(wpk, N, K)
+    _need(wpk.device == x.device, "x and the weight image must be on one device")
     _need(abits in (6, 8), "abits must be 6 or 8")
     dev = x.device
     if out is None:
         out = torch.empty((M, N), dtype=torch.float16, device=dev)
-    xq = torch.empty((M, K), dtype=torch.int8, device=dev)
-    xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=dev)
+    else:
+        _dev(out, torch.float16, "out", 2)
+        _need(tuple(out.shape) == (M, N), f"out must be [M, N] = {(M, N)}")
+    xq = xs = None
+    if act_scratch_bytes(M, N, K):  # prefill sizes quantize in a separate launch
+        xq = torch.empty((M, K), dtype=torch.int8, device=dev)
+        xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=dev)
     s = _stream(x)
     nb = gemm_workspace_bytes(M, N, K)
     wbuf = workspace(dev, nb, s.value)
-    _lib.call("fq_linear_w6ax", _ptr(x), M, N, K, abits, _ptr(wpk), _ptr(ws), _ptr(out), _ptr(xq),
+    _lib.call("fq_linear_w6ax", _ptr(x), M, N, K, abits, _ptr(wpk), _ptr(out), _ptr(xq),
               _ptr(xs), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
     return out
+
+
+def act_scratch_bytes(M, N, K):
+    """Activation scratch fq_linear_w6ax needs (0: decode sizes run as one fused launch)."""
+    return int(_lib.load().fq_linear_act_scratch_bytes(M, N, K))
 
 
 # ------------------------------------------------------------------------- reference layouts
@@ -199,13 +217,15 @@ def ref_quantize_bit_packing(x, bits):
     return planes, dup
 
 
-def import_ref_w(planes, N, K):
+def import_ref_w(planes, ws, N, K):
+    """Reference bit-plane weights + W_SCALE [K/128, N] -> weight image."""
     _dev(planes, torch.int32, "planes", 1)
     _k_ok(K)
     _rows_ok(N)
     _need(planes.numel() == 6 * N * (K // 32), "planes size does not match 6-bit [N,K]")
+    _ws_ok(ws, N, K, planes.device)
     out = torch.empty(packed_w_bytes(N, K), dtype=torch.uint8, device=planes.device)
-    _lib.call("fq_import_ref_w", _ptr(planes), N, K, _ptr(out), _stream(planes))
+    _lib.call("fq_import_ref_w", _ptr(planes), _ptr(ws), N, K, _ptr(out), _stream(planes))
     return out
 
 

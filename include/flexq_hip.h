@@ -23,9 +23,12 @@
  * Data layouts owned by this build
  *   xq   int8  [M][K]               activation codes (values in [-32,31] for A6, [-128,127] for A8)
  *   xs   fp16  [K/128][M]           activation group scales
- *   wpk  bytes fq_packed_w_bytes(N,K): "fq6" layout, 0.75 B per weight, MFMA-operand ordered
- *   ws   fp16  [K/128][N]           weight group scales (same as the reference's W_SCALE,
- *                                   test_bgemm_kernel.cu:57-63)
+ *   wpk  bytes fq_packed_w_bytes(N,K): the weight image -- 6-bit codes in "fq6" blocks (16
+ *                                   columns x one 128-group, 1.5 KiB, MFMA-operand ordered,
+ *                                   0.75 B per weight) followed by the group scales blocked the
+ *                                   same way (fp16 [N/16][K/128][16]); built once, offline
+ *   ws   fp16  [K/128][N]           weight group scales in the reference's W_SCALE layout
+ *                                   (test_bgemm_kernel.cu:57-63): an input of the packers only
  *   d    fp16  [M][N]               output, row-major
  * Reference layouts (bit planes, duplicated half2 x-scales) are accepted by the fq_ref_* and
  * fq_import_* entry points.
@@ -55,7 +58,8 @@ const char *fq_version(void);
 const char *fq_status_string(fq_status s);
 
 /* ---- sizes ------------------------------------------------------------------------------- */
-/* Bytes of the fq6 packed weight for an [N][K] matrix (N padded to 32 internally). */
+/* Bytes of the weight image for an [N][K] matrix (N padded to 16 internally): 1568 B per
+ * 16 columns x 128 k (1536 B codes + 32 B scales). */
 size_t fq_packed_w_bytes(int N, int K);
 /* Bytes of scratch fq_gemm_w6ax / fq_linear_w6ax need for this shape (0 if none).  The buffer
  * must be zero-filled once after allocation (fq_workspace_init); the kernels leave it zeroed. */
@@ -63,13 +67,16 @@ size_t fq_gemm_workspace_bytes(int M, int N, int K);
 fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_t stream);
 
 /* ---- weight packing (offline) ------------------------------------------------------------- */
-/* int8 weight codes [N][K] (values in [-32,31]) -> fq6.  Replaces flexq_bit_packing(const int*,
- * int*, M, K, BIT, stream) applied to weights (engine/src/pack/bit_packing.h:34,
- * test_bgemm_kernel.cu:222-223). */
-fq_status fq_pack_w6(const int8_t *wq, int N, int K, void *w_packed, fq_stream_t stream);
-/* Inverse, for checks: fq6 -> int8 [N][K]. */
-fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, fq_stream_t stream);
-/* fp16 weight [N][K] -> per-(row,128-group) symmetric 6-bit codes + fq6 + ws [K/128][N].
+/* int8 weight codes [N][K] (values in [-32,31]) + ws [K/128][N] -> weight image.  Replaces
+ * flexq_bit_packing(const int*, int*, M, K, BIT, stream) applied to weights
+ * (engine/src/pack/bit_packing.h:34, test_bgemm_kernel.cu:222-223); the W_SCALE the reference
+ * passes to every GEMM call is folded into the image here, once. */
+fq_status fq_pack_w6(const int8_t *wq, const uint16_t *ws, int N, int K, void *w_packed,
+                     fq_stream_t stream);
+/* Inverse, for checks: image -> int8 [N][K] (+ ws [K/128][N] when ws != NULL). */
+fq_status fq_unpack_w6(const void *w_packed, int N, int K, int8_t *wq, uint16_t *ws,
+                       fq_stream_t stream);
+/* fp16 weight [N][K] -> per-(row,128-group) symmetric 6-bit codes -> image, plus ws [K/128][N].
  * Same rounding rule as fq_quantize_act (the offline converter the reference does not ship,
  * LlamaDecoderLayerWeight.cc:381-410 loads its output). wq_out (int8 [N][K]) is optional. */
 fq_status fq_quantize_pack_w6(const uint16_t *w, int N, int K, void *w_packed, uint16_t *ws,
@@ -84,23 +91,25 @@ fq_status fq_quantize_act(const uint16_t *x, int M, int K, int abits, int8_t *xq
                           fq_stream_t stream);
 
 /* ---- GEMM ------------------------------------------------------------------------------- */
-/* d[M][N] = fp16( sum_g float(half(xs[g][m]*ws[g][n])) * acc[m][n][g] ),
+/* d[M][N] = fp16( sum_g float(half(xs[g][m]*ws[g][n])) * acc[m][n][g] ), ws from the image,
  * acc[m][n][g] = sum_{k in g} xq[m][k]*wq[n][k] (exact int32).  Replaces
  * FQBMMAInitFn/FQBMMAExecFn (engine/src/bgemm/flexq_bmma_op.h:163-188) and
  * FLEXQGEMMWrapper::gemm(int* A ...) (e2e .../flexq_gemm_wrapper.cu:21-97).
  * acc_dbg: optional int32 [M][N][K/128] copy of the group accumulators (bit-exact checks).
  * workspace: fq_gemm_workspace_bytes(M,N,K) bytes, initialised once by fq_workspace_init. */
-fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const void *w_packed,
-                       const uint16_t *ws, int M, int N, int K, int abits, uint16_t *d,
-                       int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
-                       fq_stream_t stream);
+fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N,
+                       int K, int abits, uint16_t *d, int32_t *acc_dbg, void *workspace,
+                       size_t workspace_bytes, fq_stream_t stream);
 
 /* Quantize + GEMM in one call.  Replaces FLEXQGEMMWrapper::gemm(const half* A ...)
- * (flexq_gemm_wrapper.cu:99-122).  xq_buf/xs_buf: caller scratch of M*K bytes and
+ * (flexq_gemm_wrapper.cu:99-122).  Decode sizes (M <= 32, fq_linear_act_scratch_bytes() == 0)
+ * run as ONE launch: the GEMM quantizes its activation groups itself and xq_buf/xs_buf are not
+ * touched (may be NULL).  Otherwise xq_buf/xs_buf are caller scratch of M*K bytes and
  * 2*M*(K/128) bytes (the reference's activation workspace, LlamaV2ContextAttentionLayer.cc:793). */
+size_t fq_linear_act_scratch_bytes(int M, int N, int K);
 fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
-                         const uint16_t *ws, uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf,
-                         void *workspace, size_t workspace_bytes, fq_stream_t stream);
+                         uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
+                         size_t workspace_bytes, fq_stream_t stream);
 
 /* ---- reference-layout entry points (drop-in for FlexQ's own formats) ------------------------ */
 /* flexq_bit_packing(const int* in, int* out, M, K, BIT, stream) (engine/src/pack/bit_packing.h:34,
@@ -113,9 +122,10 @@ fq_status fq_ref_bit_packing(const int32_t *in, int32_t *packed, int M, int K, i
  * pack; x_scale_dup is the reference layout half[K/128][2*ceil4(M)] of duplicated pairs. */
 fq_status fq_ref_quantize_bit_packing(const uint16_t *x, int32_t *packed, uint16_t *x_scale_dup,
                                       int M, int K, int bits, fq_stream_t stream);
-/* Reference bit-plane weights (W_BITS = 6, [K/128][N/c][6][c][4]) -> fq6. */
-fq_status fq_import_ref_w(const int32_t *w_bitplanes, int N, int K, void *w_packed,
-                          fq_stream_t stream);
+/* Reference bit-plane weights (W_BITS = 6, [K/128][N/c][6][c][4]) + W_SCALE [K/128][N] ->
+ * weight image. */
+fq_status fq_import_ref_w(const int32_t *w_bitplanes, const uint16_t *w_scale, int N, int K,
+                          void *w_packed, fq_stream_t stream);
 /* Reference bit-plane activations + duplicated scales -> xq int8 [M][K] + xs [K/128][M]. */
 fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, int M, int K,
                           int bits, int8_t *xq, uint16_t *xs, fq_stream_t stream);
@@ -123,15 +133,16 @@ fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_du
 /* FQBMMAOpState-style two-call interface over REFERENCE-layout operands
  * (flexq_bmma_op.h:19-34,163-188): init validates and records the arguments (no launch, no
  * device-attribute call per init, unlike flexq_bmma_op.h:103), exec imports X from bit planes
- * into `scratch` and runs fq_gemm_w6ax.  W must already be in fq6 (import it once with
- * fq_import_ref_w, as FT loads pre-packed weights once).  scratch: fq_bmma_scratch_bytes(). */
+ * into `scratch` and runs fq_gemm_w6ax.  W must already be a weight image (import it once with
+ * fq_import_ref_w(W planes, W_SCALE), as FT loads pre-packed weights once); the image carries
+ * the scales, so W_SCALE is recorded but not read (may be NULL).  scratch: fq_bmma_scratch_bytes(). */
 typedef struct fq_bmma_state {
     int init_success;
     int M, N, K, x_bits, w_bits, group_size;
     const int32_t *X;        /* reference bit-plane activations */
-    const void *W;           /* fq6 weights */
+    const void *W;           /* weight image */
     const uint16_t *X_SCALE; /* reference duplicated layout */
-    const uint16_t *W_SCALE; /* [K/128][N] */
+    const uint16_t *W_SCALE; /* [K/128][N], not read (the image carries the scales) */
     uint16_t *D;
     void *scratch;
     size_t scratch_bytes;

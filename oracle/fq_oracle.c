@@ -14,7 +14,7 @@
  *   fqo_gemm               the contract: int32 per-group accumulators (exact) dequantised with the
  *                          fp16-rounded scale product of flexq_bmma_kernel.h:360-364, summed in
  *                          double and rounded once to fp16.
- *   fqo_pack_fq6 / fqo_unpack_fq6   this build's own 6-bit weight layout --
+ *   fqo_pack_fq6 / fqo_unpack_fq6   this build's own 6-bit weight image --
  *                          a model of the HIP packer, not a reference function.
  *
  * Parity pinning: the reference ships no kernel golden vectors (inputs are time-seeded,
@@ -285,34 +285,43 @@ int fqo_xs_to_ref_dup(const uint16_t *xs, int M, int K, uint16_t *dup) {
 /* ---------------------------------------------------------------- this build's fq6 layout */
 
 /* Model of the HIP packer's output (flexq_amd/csrc/fq_quant.hip).  Layout:
- *   uint32 [Npad/32][K/128][3 plane r][64 lane][4 kstep s],  Npad = ceil(N/32)*32 (pad cols = 0)
- *   lane l, kstep s hold column n = 32t + (l&31), k = 128g + 32s + 16(l>>5) + j, j = 0..15;
+ *   uint32 [Npad/16][K/128][3 plane r][64 lane][2 kstep s],  Npad = ceil(N/16)*16 (pad cols = 0)
+ *   lane l, kstep s hold column n = 16t + (l&15), k = 128g + 64s + 16(l>>4) + j, j = 0..15
+ *   (the B operand of v_mfma_i32_16x16x64_i8 for k-step s);
  *   byte b of word (r, s): ((v[4r+b] & 63) << 2) | ((v[12+b] >> 2r) & 3).
- * A (tile, group) block is 3 KiB = three 1 KiB planes; lane l's plane r is 16 contiguous bytes,
- * so one dwordx4 / LDS-DMA wave instruction moves one plane.  Unpacking (out_r = P_r &
- * 0xFCFCFCFC, out_3 = sum_r (P_r & 0x03030303) << (2r+2)) yields 4*v as int8: the MFMA B
- * operand scaled by 4. */
-size_t fqo_fq6_bytes(int N, int K) { return (size_t)((N + 31) / 32) * (K / 128) * 3072; }
+ * A (16-column tile, group) block is 1.5 KiB = three 512 B planes; lane l's plane r is 8
+ * contiguous bytes (both k-steps).  Unpacking (out_r = P_r & 0xFCFCFCFC, out_3 = sum_r
+ * (P_r & 0x03030303) << (2r+2)) yields 4*v as int8: the MFMA B operand scaled by 4.
+ * The image ends with the group scales blocked the same way: fp16 [Npad/16][K/128][16] at byte
+ * offset Npad/16 * K/128 * 1536 (pad columns 0), 32 contiguous bytes per block. */
+size_t fqo_fq6_bytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / 128) * (1536 + 32); }
+
+static inline size_t fq6_scale_index(int t, int g, int c, int G) { return ((size_t)t * G + g) * 16 + c; }
 
 static inline size_t fq6_word(int t, int g, int r, int l, int s, int G) {
-    return ((((size_t)t * G + g) * 3 + r) * 64 + l) * 4 + s;
+    return ((((size_t)t * G + g) * 3 + r) * 64 + l) * 2 + s;
 }
 
-int fqo_pack_fq6(const int8_t *wq, int N, int K, uint8_t *out) {
+static inline int fq6_col(int t, int l) { return 16 * t + (l & 15); }
+static inline int fq6_k(int g, int s, int l, int j) { return 128 * g + 64 * s + 16 * (l >> 4) + j; }
+
+int fqo_pack_fq6(const int8_t *wq, const uint16_t *ws, int N, int K, uint8_t *out) {
     if (N <= 0 || K % 128 != 0) return 1;
-    const int NT = (N + 31) / 32, G = K / 128;
+    const int NT = (N + 15) / 16, G = K / 128;
     uint32_t *o = (uint32_t *)out;
+    uint16_t *sc = (uint16_t *)(out + (size_t)NT * G * 1536);
     memset(out, 0, fqo_fq6_bytes(N, K));
     for (int t = 0; t < NT; t++)
         for (int g = 0; g < G; g++)
-            for (int s = 0; s < 4; s++)
+            for (int c = 0; c < 16; c++)
+                if (16 * t + c < N) sc[fq6_scale_index(t, g, c, G)] = ws[(size_t)g * N + 16 * t + c];
+    for (int t = 0; t < NT; t++)
+        for (int g = 0; g < G; g++)
+            for (int s = 0; s < 2; s++)
                 for (int l = 0; l < 64; l++) {
-                    int n = 32 * t + (l & 31);
+                    int n = fq6_col(t, l);
                     int v[16];
-                    for (int j = 0; j < 16; j++) {
-                        int k = 128 * g + 32 * s + 16 * (l >> 5) + j;
-                        v[j] = (n < N) ? wq[(size_t)n * K + k] : 0;
-                    }
+                    for (int j = 0; j < 16; j++) v[j] = (n < N) ? wq[(size_t)n * K + fq6_k(g, s, l, j)] : 0;
                     for (int r = 0; r < 3; r++) {
                         uint32_t w = 0;
                         for (int b = 0; b < 4; b++)
@@ -324,20 +333,23 @@ int fqo_pack_fq6(const int8_t *wq, int N, int K, uint8_t *out) {
     return 0;
 }
 
-int fqo_unpack_fq6(const uint8_t *packed, int N, int K, int8_t *wq) {
+int fqo_unpack_fq6(const uint8_t *packed, int N, int K, int8_t *wq, uint16_t *ws) {
     if (N <= 0 || K % 128 != 0) return 1;
-    const int NT = (N + 31) / 32, G = K / 128;
+    const int NT = (N + 15) / 16, G = K / 128;
     const uint32_t *p = (const uint32_t *)packed;
+    const uint16_t *sc = (const uint16_t *)(packed + (size_t)NT * G * 1536);
+    if (ws)
+        for (int g = 0; g < G; g++)
+            for (int n = 0; n < N; n++) ws[(size_t)g * N + n] = sc[fq6_scale_index(n / 16, g, n % 16, G)];
     for (int t = 0; t < NT; t++)
         for (int g = 0; g < G; g++)
-            for (int s = 0; s < 4; s++)
+            for (int s = 0; s < 2; s++)
                 for (int l = 0; l < 64; l++) {
-                    int n = 32 * t + (l & 31);
+                    int n = fq6_col(t, l);
                     if (n >= N) continue;
                     uint32_t w[3];
                     for (int r = 0; r < 3; r++) w[r] = p[fq6_word(t, g, r, l, s, G)];
                     for (int j = 0; j < 16; j++) {
-                        int k = 128 * g + 32 * s + 16 * (l >> 5) + j;
                         unsigned u;
                         if (j < 12) {
                             u = ((w[j / 4] >> (8 * (j % 4))) & 0xffu) >> 2;
@@ -346,7 +358,7 @@ int fqo_unpack_fq6(const uint8_t *packed, int N, int K, int8_t *wq) {
                             u = 0;
                             for (int r = 0; r < 3; r++) u |= ((w[r] >> (8 * b)) & 3u) << (2 * r);
                         }
-                        wq[(size_t)n * K + k] = (int8_t)((int)(u << 26) >> 26);
+                        wq[(size_t)n * K + fq6_k(g, s, l, j)] = (int8_t)((int)(u << 26) >> 26);
                     }
                 }
     return 0;

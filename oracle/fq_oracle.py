@@ -42,8 +42,8 @@ def lib():
             "fqo_compute_ref": [P, P, P, P, P, I, I, I, I, I],
             "fqo_gemm": [P, P, P, P, I, I, I, P, P, P],
             "fqo_xs_to_ref_dup": [P, I, I, P],
-            "fqo_pack_fq6": [P, I, I, P],
-            "fqo_unpack_fq6": [P, I, I, P],
+            "fqo_pack_fq6": [P, P, I, I, P],
+            "fqo_unpack_fq6": [P, I, I, P, P],
         }.items():
             fn = getattr(L, name)
             fn.argtypes = args
@@ -138,18 +138,26 @@ def fq6_bytes(N, K):
     return int(lib().fqo_fq6_bytes(N, K))
 
 
-def pack_fq6(wq):
+def pack_fq6(wq, ws=None):
+    """Weight image: fq6 blocks + blocked fp16 scales (ws [K/128, N]; zeros if None)."""
     wq = np.ascontiguousarray(wq, dtype=np.int8)
     N, K = wq.shape
+    if ws is None:
+        ws = np.zeros((K // 128, N), np.float16)
+    ws = np.ascontiguousarray(ws, dtype=np.float16)
+    assert ws.shape == (K // 128, N)
     out = np.zeros(fq6_bytes(N, K), dtype=np.uint8)
-    _check(lib().fqo_pack_fq6(_p(wq), N, K, _p(out)), "pack_fq6")
+    _check(lib().fqo_pack_fq6(_p(wq), _p(ws), N, K, _p(out)), "pack_fq6")
     return out
 
 
-def unpack_fq6(packed, N, K):
+def unpack_fq6(packed, N, K, want_ws=False):
     wq = np.zeros((N, K), dtype=np.int8)
-    _check(lib().fqo_unpack_fq6(_p(np.ascontiguousarray(packed, dtype=np.uint8)), N, K, _p(wq)),
+    ws = np.zeros((K // 128, N), dtype=np.float16)
+    _check(lib().fqo_unpack_fq6(_p(np.ascontiguousarray(packed, dtype=np.uint8)), N, K, _p(wq), _p(ws)),
            "unpack_fq6")
+    if want_ws:
+        return wq, ws
     return wq
 
 

@@ -4,7 +4,7 @@ Bit-exact: activation codes + scales, fq6 packing, reference bit planes, imports
 group accumulators.  fp16 outputs: within 1e-3 relative + the fp32-accumulation floor
 (oracle.gemm_tolerance).  Shapes cover the reference's edge cases: M in {1,2,4,8} (the wrapper's
 buckets, flexq_gemm_wrapper.cu:53-84) and the ragged ones the reference gets wrong (3, 5-7,
-M % 8 != 0), N not a multiple of 32, K = 128 (minimum) and K = 11008 (86 groups, odd split),
+M % 8 != 0), N not a multiple of 16, K = 128 (minimum) and K = 11008 (86 groups, odd split),
 all-zero groups, tiny/huge groups, and the A8 range.
 """
 import numpy as np
@@ -61,14 +61,57 @@ def test_quantize_act_edge_cases(ops, dev, bits):
     np.testing.assert_array_equal(host(xq), oracle.quantize_engine(x, 6)[0])
 
 
+def tie_heavy_input(M, K, bits, seed):
+    """Groups whose scale is exactly a power of two s (absmax = (2^(b-1)-1) s), every other value
+    an integer multiple of s/2: about half the quotients are exact .5 ties, the rest exact
+    integers -- the cases where a division shortcut could round differently."""
+    r = rng(seed)
+    hi = (1 << (bits - 1)) - 1
+    e = r.integers(-20, 9, size=(M, K // 128, 1))
+    s = np.ldexp(1.0, e)
+    m = r.integers(-2 * hi, 2 * hi + 1, size=(M, K // 128, 128)).astype(np.float64)
+    x = m * s / 2
+    x[:, :, 0] = hi * s[:, :, 0] * np.where(r.random((M, K // 128)) < 0.5, 1, -1)
+    # plus non-tie values in some groups: odd multiples of s/1024
+    noisy = r.random((M, K // 128)) < 0.25
+    x[noisy, 1:] += (r.integers(-5, 6, size=(int(noisy.sum()), 127)) * 2 + 1) * s[noisy][:, :1] / 1024
+    out = x.reshape(M, K).astype(np.float16)
+    return out
+
+
+@pytest.mark.parametrize("bits", [6, 8])
+def test_quantize_act_tie_stress(ops, dev, bits):
+    """Quotient-rounding stress: exact ties and exact integers across scales 2^-20 .. 2^8."""
+    x = tie_heavy_input(64, 2048, bits, seed=bits)
+    xq, xs = ops.quantize_act(to_dev(x, dev), bits)
+    q_ref, xs_ref = oracle.quantize_engine(x, bits)
+    np.testing.assert_array_equal(host(xs).view(np.uint16), xs_ref.view(np.uint16))
+    np.testing.assert_array_equal(host(xq), q_ref)
+    # the fused decode quantizer is the same code path: same codes through the GEMM result
+    N = 64
+    r = rng(5)
+    wq = r.integers(-32, 32, size=(N, 2048)).astype(np.int8)
+    ws = (r.random((16, N)) * 0.05).astype(np.float16)
+    pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+    for M in (1, 4, 16):
+        d = ops.linear_w6ax(to_dev(x[:M], dev), pk, N, bits)
+        d2 = ops.gemm_w6ax(to_dev(q_ref[:M], dev), to_dev(np.ascontiguousarray(xs_ref[:, :M]), dev), pk, N, bits)
+        np.testing.assert_array_equal(host(d).view(np.uint16), host(d2).view(np.uint16))
+
+
 # ------------------------------------------------------------------ packers and importers
 
-@pytest.mark.parametrize("N,K", [(32, 128), (64, 4096), (40, 384), (4096, 256)])
+@pytest.mark.parametrize("N,K", [(32, 128), (64, 4096), (40, 384), (4096, 256), (17, 128), (8, 256)])
 def test_pack_w6_bit_exact(ops, dev, N, K):
-    wq = rng(N * 7 + K).integers(-32, 32, size=(N, K)).astype(np.int8)
-    pk = ops.pack_w6(to_dev(wq, dev))
-    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq))
-    np.testing.assert_array_equal(host(ops.unpack_w6(pk, N, K)), wq)
+    """Weight image (codes + blocked scales) byte-identical to the oracle's, and it round-trips."""
+    r = rng(N * 7 + K)
+    wq = r.integers(-32, 32, size=(N, K)).astype(np.int8)
+    ws = (r.random((K // 128, N)) * 0.05).astype(np.float16)
+    pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq, ws))
+    wq2, ws2 = ops.unpack_w6(pk, N, K)
+    np.testing.assert_array_equal(host(wq2), wq)
+    np.testing.assert_array_equal(host(ws2).view(np.uint16), ws.view(np.uint16))
 
 
 @pytest.mark.parametrize("N,K", [(32, 128), (96, 1024), (40, 256)])
@@ -78,7 +121,7 @@ def test_quantize_pack_w6(ops, dev, N, K):
     wq_ref, ws_ref = oracle.quantize_engine(w, 6)
     np.testing.assert_array_equal(host(wq), wq_ref)
     np.testing.assert_array_equal(host(ws).view(np.uint16), ws_ref.view(np.uint16))
-    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq_ref))
+    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq_ref, ws_ref))
 
 
 @pytest.mark.parametrize("R,K,bits", [(1, 128, 6), (4, 512, 8), (8, 256, 6), (24, 384, 6), (16, 128, 8)])
@@ -105,17 +148,18 @@ def test_ref_quantize_bit_packing(ops, dev, M, K, bits):
 def test_import_ref_w(ops, dev, N, K):
     wraw = rng(N + K).integers(0, 64, size=(N, K), dtype=np.int32)
     wq = ((wraw ^ 32) - 32).astype(np.int8)
+    ws = (rng(K).random((K // 128, N)) * 0.1).astype(np.float16)
     planes = oracle.pack_bitplanes(wraw, 6)
-    pk = ops.import_ref_w(to_dev(planes, dev), N, K)
-    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq))
+    pk = ops.import_ref_w(to_dev(planes, dev), to_dev(ws, dev), N, K)
+    np.testing.assert_array_equal(host(pk), oracle.pack_fq6(wq, ws))
 
 
 # ------------------------------------------------------------------ GEMM
 
 def run_gemm(ops, dev, xq, xs, wq, ws, abits):
     N = wq.shape[0]
-    pk = ops.pack_w6(to_dev(wq, dev))
-    args = (to_dev(xq, dev), to_dev(xs, dev), pk, to_dev(ws, dev), N, abits)
+    pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+    args = (to_dev(xq, dev), to_dev(xs, dev), pk, N, abits)
     d, acc = ops.gemm_w6ax(*args, return_acc=True)
     d_prod = ops.gemm_w6ax(*args)  # the production (no debug output) kernel variant
     np.testing.assert_array_equal(host(d).view(np.uint16), host(d_prod).view(np.uint16))
@@ -166,24 +210,28 @@ def test_gemm_zero_groups_and_extremes(ops, dev):
 
 def test_gemm_deterministic(ops, dev):
     _, _, xq, wq, xs, ws = kat_operands(1, 4096, 4096, 6, seed=5)
-    pk = ops.pack_w6(to_dev(wq, dev))
-    a = [host(ops.gemm_w6ax(to_dev(xq, dev), to_dev(xs, dev), pk, to_dev(ws, dev), 4096, 6)) for _ in range(3)]
+    pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+    a = [host(ops.gemm_w6ax(to_dev(xq, dev), to_dev(xs, dev), pk, 4096, 6)) for _ in range(3)]
     for b in a[1:]:
         np.testing.assert_array_equal(a[0].view(np.uint16), b.view(np.uint16))
 
 
-@pytest.mark.parametrize("M,N,K,abits", [(1, 28672, 8192, 6), (8, 8192, 28672, 6), (16, 24576, 8192, 6)])
+@pytest.mark.parametrize("M,N,K,abits", [
+    (1, 28672, 8192, 6), (8, 8192, 28672, 6), (16, 24576, 8192, 6),  # LLaMA-2-70B (BASELINE C4)
+    # long K / many tiles per CU: the staging variants (activations, then scales, in the ring)
+    (16, 8192, 28672, 6), (32, 28672, 8192, 8), (4, 8192, 65536, 6), (12, 16384, 16384, 8), (1, 57344, 8192, 6),
+])
 def test_gemm_full_size_sampled_columns(ops, dev, M, N, K, abits):
-    """BASELINE sizes (LLaMA-2-70B): the whole GEMM runs on the GPU, the oracle checks a seeded
-    sample of 96 columns exactly (accumulators) and within tolerance (outputs)."""
+    """Full sizes: the whole GEMM runs on the GPU, the oracle checks a seeded sample of 96
+    columns exactly (accumulators) and within tolerance (outputs)."""
     r = rng(N + K)
     xq = r.integers(-(1 << (abits - 1)), 1 << (abits - 1), size=(M, K)).astype(np.int8)
     wq_dev = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev,
                            generator=torch.Generator(device=dev).manual_seed(7))
     xs = (r.random((K // 128, M)) * 0.05).astype(np.float16)
     ws = (r.random((K // 128, N)) * 0.05).astype(np.float16)
-    pk = ops.pack_w6(wq_dev)
-    d, acc = ops.gemm_w6ax(to_dev(xq, dev), to_dev(xs, dev), pk, to_dev(ws, dev), N, abits, return_acc=True)
+    pk = ops.pack_w6(wq_dev, to_dev(ws, dev))
+    d, acc = ops.gemm_w6ax(to_dev(xq, dev), to_dev(xs, dev), pk, N, abits, return_acc=True)
     cols = np.sort(r.choice(N, size=96, replace=False))
     cols_t = torch.from_numpy(cols).to(dev)
     wq_s = host(wq_dev.index_select(0, cols_t))
@@ -191,16 +239,58 @@ def test_gemm_full_size_sampled_columns(ops, dev, M, N, K, abits):
     np.testing.assert_array_equal(host(acc.index_select(1, cols_t)), acc_ref)
     assert_gemm_close(host(d)[:, cols], ref, mag, f"full-size M={M} N={N} K={K}")
     # the packed weight round-trips at full size
-    assert torch.equal(ops.unpack_w6(pk, N, K), wq_dev)
+    assert torch.equal(ops.unpack_w6(pk, N, K)[0], wq_dev)
 
 
-def test_linear_matches_quantize_then_gemm(ops, dev):
-    M, N, K = 16, 4096, 4096
-    x, w, xq, wq, xs, ws = model_operands(M, N, K, 6, seed=9)
-    pk = ops.pack_w6(to_dev(wq, dev))
-    d = host(ops.linear_w6ax(to_dev(x, dev), pk, to_dev(ws, dev), N, 6))
+LINEAR_SHAPES = [
+    # (M, N, K, abits): decode sizes run fused (one launch), the rest quantize separately
+    (1, 4096, 4096, 6), (1, 12288, 4096, 6), (1, 100, 384, 6), (1, 4096, 11008, 8), (2, 33, 128, 6),
+    (3, 512, 1024, 8), (4, 11008, 4096, 6), (5, 64, 256, 6), (8, 1024, 4096, 6), (9, 96, 1280, 8),
+    (16, 4096, 4096, 6), (16, 11008, 4096, 6), (16, 4096, 11008, 8), (17, 256, 1024, 6),
+    (32, 4096, 4096, 8), (33, 128, 512, 6), (64, 256, 1024, 8),
+]
+
+
+@pytest.mark.parametrize("M,N,K,abits", LINEAR_SHAPES)
+def test_linear_matches_quantize_then_gemm(ops, dev, M, N, K, abits):
+    """fq_linear_w6ax (FLEXQGEMMWrapper::gemm(const half* A ...)): bit-identical to the two-launch
+    quantize + GEMM path, whichever of the two it takes, and within tolerance of the oracle."""
+    x, w, xq, wq, xs, ws = model_operands(M, N, K, abits, seed=M * 7 + N + K)
+    pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+    xd = to_dev(x, dev)
+    d = ops.linear_w6ax(xd, pk, N, abits)
+    xq_d, xs_d = ops.quantize_act(xd, abits)
+    d2 = ops.gemm_w6ax(xq_d, xs_d, pk, N, abits)
+    np.testing.assert_array_equal(host(d).view(np.uint16), host(d2).view(np.uint16))
     ref, _, mag = oracle.gemm(xq, xs, wq, ws)
-    assert_gemm_close(d, ref, mag, "linear")
+    assert_gemm_close(host(d), ref, mag, f"linear M={M} N={N} K={K}")
+
+
+def test_linear_fuses_at_decode_sizes(ops):
+    """The BASELINE decode shapes run as one launch (no activation scratch needed)."""
+    for (N, K) in [(12288, 4096), (4096, 4096), (11008, 4096), (4096, 11008), (28672, 8192), (8192, 28672)]:
+        assert ops.act_scratch_bytes(1, N, K) == 0, (N, K)
+    assert ops.act_scratch_bytes(16, 11008, 4096) == 0
+    assert ops.act_scratch_bytes(33, 4096, 4096) == 33 * 4096 + 33 * 32 * 2
+
+
+def test_linear_edge_inputs(ops, dev):
+    """Fused quantizer on the edge groups (zeros, ties, outliers, tiny values)."""
+    for name, x in edge_inputs().items():
+        x = np.ascontiguousarray(x.reshape(-1, x.shape[-1]).astype(np.float16))
+        M, K = x.shape
+        if K % 128 or M > 32:
+            continue
+        N = 96
+        r = rng(M + K)
+        wq = r.integers(-32, 32, size=(N, K)).astype(np.int8)
+        ws = (r.random((K // 128, N)) * 0.05).astype(np.float16)
+        pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+        for abits in (6, 8):
+            d = ops.linear_w6ax(to_dev(x, dev), pk, N, abits)
+            xq, xs = oracle.quantize_engine(x, abits)
+            ref, _, mag = oracle.gemm(xq, xs, wq, ws)
+            assert_gemm_close(host(d), ref, mag, f"linear edge {name} a{abits}")
 
 
 def test_bmma_state_api_reference_layout(ops, dev):
@@ -210,7 +300,7 @@ def test_bmma_state_api_reference_layout(ops, dev):
     M, N, K, abits = 4, 256, 1024, 6
     xraw, wraw, xq, wq, xs, ws = kat_operands(M, N, K, abits, seed=77)
     X = to_dev(oracle.pack_bitplanes(xraw, abits), dev)
-    W = ops.import_ref_w(to_dev(oracle.pack_bitplanes(wraw, 6), dev), N, K)
+    W = ops.import_ref_w(to_dev(oracle.pack_bitplanes(wraw, 6), dev), to_dev(ws, dev), N, K)
     XS = to_dev(oracle.xs_to_ref_dup(xs, M, K), dev)
     WS = to_dev(ws, dev)
     D = torch.empty((M, N), dtype=torch.float16, device=dev)

@@ -103,27 +103,37 @@ def test_bitplane_rejects_hazard_rows():
         oracle.pack_bitplanes(np.zeros((12, 128), np.int32), 6)
 
 
-@pytest.mark.parametrize("N,K", [(32, 128), (64, 384), (40, 256), (1, 128)])
+@pytest.mark.parametrize("N,K", [(32, 128), (64, 384), (40, 256), (1, 128), (17, 128)])
 def test_fq6_roundtrip(N, K):
-    wq = rng(N + K).integers(-32, 32, size=(N, K)).astype(np.int8)
-    pk = oracle.pack_fq6(wq)
-    assert pk.size == ((N + 31) // 32) * (K // 128) * 3072
-    np.testing.assert_array_equal(oracle.unpack_fq6(pk, N, K), wq)
+    r = rng(N + K)
+    wq = r.integers(-32, 32, size=(N, K)).astype(np.int8)
+    ws = (r.random((K // 128, N)) * 0.1).astype(np.float16)
+    pk = oracle.pack_fq6(wq, ws)
+    assert pk.size == ((N + 15) // 16) * (K // 128) * (1536 + 32)  # codes + blocked scales
+    wq2, ws2 = oracle.unpack_fq6(pk, N, K, want_ws=True)
+    np.testing.assert_array_equal(wq2, wq)
+    np.testing.assert_array_equal(ws2.view(np.uint16), ws.view(np.uint16))
+    # the scale region: fp16 [N/16][K/128][16], pad columns 0
+    sc = pk[((N + 15) // 16) * (K // 128) * 1536:].view(np.uint16).reshape((N + 15) // 16, K // 128, 16)
+    assert sc[0, 0, 0] == ws.view(np.uint16)[0, 0]
+    if N % 16:
+        assert np.all(sc[-1, :, N % 16:] == 0)
 
 
 def test_fq6_unpack_rule_gives_4w():
     """The documented register unpack (out_r = P_r & 0xFC.., out_3 from the low bit pairs) yields
-    4*w per byte for every lane and k-step of one (tile, group) block [3 planes][64 lanes][4 steps]."""
-    wq = rng(3).integers(-32, 32, size=(32, 128)).astype(np.int8)
-    pk = oracle.pack_fq6(wq).view(np.uint32).reshape(3, 64, 4)
-    for s in range(4):
+    4*w per byte for every lane and k-step of one (tile, group) block [3 planes][64 lanes][2 steps]:
+    lane l, step s = the v_mfma_i32_16x16x64_i8 B operand, column l&15, k = 64s + 16(l>>4) + j."""
+    wq = rng(3).integers(-32, 32, size=(16, 128)).astype(np.int8)
+    pk = oracle.pack_fq6(wq)[:1536].view(np.uint32).reshape(3, 64, 2)
+    for s in range(2):
         for lane in range(64):
             p0, p1, p2 = (int(pk[r, lane, s]) for r in range(3))
             o = [p0 & 0xFCFCFCFC, p1 & 0xFCFCFCFC, p2 & 0xFCFCFCFC,
                  ((p0 & 0x03030303) << 2) | ((p1 & 0x03030303) << 4) | ((p2 & 0x03030303) << 6)]
             bts = np.frombuffer(np.array(o, dtype=np.uint32).tobytes(), dtype=np.int8)
-            n = lane & 31
-            k0 = 32 * s + 16 * (lane >> 5)
+            n = lane & 15
+            k0 = 64 * s + 16 * (lane >> 4)
             np.testing.assert_array_equal(bts.astype(np.int32), 4 * wq[n, k0:k0 + 16].astype(np.int32))
 
 

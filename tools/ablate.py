@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "tools", "libflexq_hip_abl.so")
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [(12288, 4096), (4096, 4096), (11008, 4096), (4096, 11008), (28672, 8192), (8192, 28672)]
@@ -23,27 +23,33 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     R, COPIES = 20, 6
     masks = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,2,4,6").split(",")]
+    linear = len(sys.argv) > 2 and sys.argv[2] == "linear"  # fused quantize+GEMM from fp16 x
     stream = torch.cuda.Stream()
     for (N, K) in SHAPES:
         copies = []
         for _ in range(COPIES):
             wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
-            copies.append((ops.pack_w6(wq), (torch.rand((K // 128, N), device=dev, generator=g) * 0.01).half()))
+            copies.append(ops.pack_w6(wq, (torch.rand((K // 128, N), device=dev, generator=g) * 0.01).half()))
         x = torch.randn((1, K), device=dev, dtype=torch.float16, generator=g)
         xq, xs = ops.quantize_act(x, 6)
         out = torch.empty((1, N), device=dev, dtype=torch.float16)
+
+        def run(c):
+            if linear:
+                ops.linear_w6ax(x, c, N, 6, out=out)
+            else:
+                ops.gemm_w6ax(xq, xs, c, N, 6, out=out)
         line = f"N={N:6d} K={K:6d} MB={N * K * 0.75 / 2**20:6.1f}:"
         for m in masks:
             os.environ["FQ_DEV_ABLATION"] = str(m)
             with torch.cuda.stream(stream):
                 for i in range(COPIES):
-                    ops.gemm_w6ax(xq, xs, copies[i][0], copies[i][1], N, 6, out=out)
+                    run(copies[i])
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
                 for i in range(R):
-                    pk, ws = copies[i % COPIES]
-                    ops.gemm_w6ax(xq, xs, pk, ws, N, 6, out=out)
+                    run(copies[i % COPIES])
             for _ in range(3):
                 graph.replay()
             torch.cuda.synchronize()
