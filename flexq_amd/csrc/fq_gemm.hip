@@ -178,13 +178,18 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int items = NT * S;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nit = (items - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1
-    // k-split z is the same for all of this WG's items (the grid is a multiple of S)
-    const int z = (int)blockIdx.x % S;
-    const int gz0 = (int)((long)z * G / S), gz1 = (int)((long)(z + 1) * G / S);
+    // All index math is 32-bit and divides at most once per launch (64-bit or per-item divisions
+    // cost microseconds of scalar code before the first DMA).  The grid is a multiple of S, so a
+    // WG's k-split z is fixed and its items' tiles are t0, t0 + tstep, ...
+    const int bid = blockIdx.x, grid = gridDim.x;
+    const int nit = (unsigned)(items - bid + grid - 1) / (unsigned)grid;  // >= 1
+    const int z = S == 1 ? 0 : (unsigned)bid % (unsigned)S;
+    const int t0 = S == 1 ? bid : (unsigned)bid / (unsigned)S, tstep = S == 1 ? grid : (unsigned)grid / (unsigned)S;
+    const int gz0 = S == 1 ? 0 : (unsigned)(z * G) / (unsigned)S;
+    const int gz1 = S == 1 ? G : (unsigned)((z + 1) * G) / (unsigned)S;
     const int Gz = gz1 - gz0;
     const int ngmax = (Gz + NW - 1) / NW;
-    const int ga = gz0 + (int)((long)wid * Gz / NW), gb = gz0 + (int)((long)(wid + 1) * Gz / NW);
+    const int ga = gz0 + (wid * Gz) / NW, gb = gz0 + ((wid + 1) * Gz) / NW;
     const int ng = gb - ga;  // groups per item for this wave (may be 0)
     const int n = ng * nit;  // blocks in this wave's sequence
     // blocked w-scales of the image: fp16 [NT][G][16] after the weight blocks (fq_quant.hip)
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     float *red = reinterpret_cast<float *>(smem + NW * wl);           // [RC][NW][M*16]
     int *flag = reinterpret_cast<int *>(red + RC * NW * EM);          // [IPW]
 
-    auto item_tile = [&](int it) { return ((int)blockIdx.x + it * (int)gridDim.x) / S; };
+    auto item_tile = [&](int it) { return t0 + it * tstep; };
 
     // Fused quantizer.  The fp16 activations of the wave's (group, row) pairs come in by LDS-DMA
     // (one 1 KiB instruction per 4 pairs) into a window of xwin pairs, issued ahead of the ring
@@ -259,8 +264,8 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
 
     // ---- the ring over the wave's block sequence
     const char *wbytes = reinterpret_cast<const char *>(wpk) + lane * 16;
-    auto issue = [&](int i, int slot) {
-        const int t = item_tile(i / ng), g = ga + i % ng;
+    auto issue = [&](int it, int j, int slot) {  // block (item it, group ga + j) -> slot
+        const int t = item_tile(it), g = ga + j;
         char *dst = ring + slot * C::SLOT;
         const char *src = wbytes + ((long)t * G + g) * FQ_BLOCK;
         __builtin_amdgcn_global_load_lds(src, LDS_PTR(dst), 16, 0, 2 /*nt*/);
@@ -283,9 +288,16 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     // then `vmcnt(D*U)`: everything younger is the ring.  (Each wave instruction costs the CU's
     // address unit ~30 cycles whatever its size, so only instructions that carry data are issued.)
     if (FUSE && n > 0) x_fetch(0);
+    int rit = 0, rj = 0;  // (item, group) of the next block to issue
     if (n > 0) {
 #pragma unroll
-        for (int i = 0; i < D; i++) issue(i < n ? i : n - 1, i);
+        for (int i = 0; i < D; i++) {
+            issue(rit, rj, i);
+            if (i + 1 < n && ++rj == ng) {  // (a short sequence re-issues its last block)
+                rj = 0;
+                ++rit;
+            }
+        }
     }
     FQ_STAMP(1);
 
@@ -341,7 +353,13 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             // every read has landed, and the slot's bytes are in registers before its refill
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            if (i + D < n) issue(i + D, slot);
+            if (i + D < n) {  // refill: block i + D
+                issue(rit, rj, slot);
+                if (++rj == ng) {
+                    rj = 0;
+                    ++rit;
+                }
+            }
 
             if (ABL & 2) {
                 cur[0][0] += (float)(p0[0] ^ p1[1] ^ p2[0] ^ a[0][1][0]) + (float)wsv + (float)xd[0][0];
