@@ -4,8 +4,11 @@ Workload (BASELINE.json configs[1]): LLaMA-2-7B, every linear layer of all 32 de
 W6A6 group 128, batch 1 (M = 1), random-init weights of that architecture, synthetic fp16
 activations resident in HBM.  One "step" = one token through the 32-layer linear stack: per
 layer 5 W6A6 linears (qkv 12288x4096, o 4096x4096, gate/up 11008x4096 reading the same input,
-down 4096x11008), each one fq_linear_w6ax call = dynamic activation quantization + GEMM +
-dequant (at decode sizes a single fused launch), captured into one HIP graph.
+down 4096x11008), each an fq_linear_w6ax call = dynamic activation quantization + GEMM + dequant
+(at decode sizes a single fused launch), captured into one HIP graph.  gate and up share their
+input, so by default they run as one linear over the concatenated weight image [gate; up]
+(22016x4096, output [gate | up], per-column arithmetic unchanged): 4 launches per layer
+(--no-merge: 5).
 
 Multi-GPU (torchrun, one process per GPU, RCCL): column-parallel N-shard of every linear, each
 rank packs and streams only its N/P rows, then ONE all-gather per linear of the dequantized
@@ -47,9 +50,6 @@ CONFIGS = {
 }
 
 
-LINEARS = ("qkv", "o", "gate", "up", "down")
-
-
 def alg_bytes(M, N, K, abits, fused=True):
     """Algorithmic HBM bytes of one linear launch: packed W (0.75 B/w) + W
     scales (2 B per 128 weights, inside the weight image) + the activations + fp16 D.  Fused (decode) launches read fp16 x (2 B/elem) and quantize
@@ -58,13 +58,30 @@ def alg_bytes(M, N, K, abits, fused=True):
     return N * K * 6 // 8 + 2 * N * K // GROUP + act + 2 * M * N
 
 
-def build_stack(cfg, rank, world, dev, seed=1234):
+def launch_list(lins, merge):
+    """The step's launches: (name, N, K, abits).  merge: gate and up, which read the same input,
+    run as one linear over their concatenated weights (one image [2N, K]; output [gate | up])."""
+    if not merge:
+        return list(lins)
+    out, gate = [], None
+    for (name, N, K, abits) in lins:
+        if name == "gate":
+            gate = (N, K, abits)
+        elif name == "up":
+            assert gate and gate[1] == K and gate[2] == abits
+            out.append(("gate_up", gate[0] + N, K, abits))
+        else:
+            out.append((name, N, K, abits))
+    return out
+
+
+def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
     layers, M, lins, _ = cfg
     g = torch.Generator(device=dev).manual_seed(seed + rank)
     stack = []
     for _ in range(layers):
         L = {}
-        for (name, N, K, abits) in lins:
+        for (name, N, K, abits) in launch_list(lins, merge):
             assert N % (16 * world) == 0, f"{name}: N={N} not divisible into 16-column shards for {world} ranks"
             Nl = N // world
             wq = torch.randint(-32, 32, (Nl, K), dtype=torch.int8, device=dev, generator=g)
@@ -75,9 +92,9 @@ def build_stack(cfg, rank, world, dev, seed=1234):
             full = torch.empty((world * M * Nl,), dtype=torch.float16, device=dev) if world > 1 else None
             L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full)
         # synthetic fp16 inputs of each linear (attention / activation outputs are out of scope)
-        for name in ("qkv", "o", "gate", "down"):
-            K = L[name]["K"]
-            L[name]["x"] = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+        for name in L:
+            if name != "up":  # up reads gate's input
+                L[name]["x"] = torch.randn((M, L[name]["K"]), dtype=torch.float16, device=dev, generator=g)
         stack.append(L)
     return stack
 
@@ -87,8 +104,7 @@ def run_step(stack, M, world, group=None, gather=True):
     quantize+GEMM launch each; gate and up read the same input), then one RCCL all-gather of the
     fp16 shard outputs per linear when world > 1."""
     for L in stack:
-        for name in LINEARS:
-            p = L[name]
+        for name, p in L.items():
             x = L["gate" if name == "up" else name]["x"]
             ops.linear_w6ax(x, p["pk"], p["Nl"], p["abits"], out=p["out"])
             if world > 1 and gather:
@@ -187,6 +203,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="llama2-7b-m1", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph")
+    ap.add_argument("--no-merge", action="store_true",
+                    help="launch gate and up separately (default: one linear over their concatenated weights)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline (0 = skip)")
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
@@ -203,7 +221,9 @@ def main():
 
     cfg = CONFIGS[a.config]
     layers, M, lins, desc = cfg
-    stack = build_stack(cfg, rank, world, dev)
+    merge = not a.no_merge
+    launch_lins = launch_list(lins, merge)
+    stack = build_stack(cfg, rank, world, dev, merge)
     stream = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
 
@@ -256,10 +276,11 @@ def main():
         g2.replay()
     torch.cuda.synchronize()
     t_g = time_graph(g2, a.roofline_reps, stream)
-    launches = layers * len(lins)
+    launches = layers * len(launch_lins)
     per_launch_s = t_g / (a.roofline_reps * launches)
-    fused = {(N, K): ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in lins}
-    bytes_launch = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)]) for (_, N, K, ab) in lins) / launches
+    fused = {(N, K): ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in launch_lins}
+    bytes_launch = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)])
+                                for (_, N, K, ab) in launch_lins) / launches
     achieved = bytes_launch / per_launch_s / 1e9
     del g2
 
@@ -283,6 +304,7 @@ def main():
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
             "parallelism": f"tp{world} column-parallel + RCCL all-gather per linear" if world > 1 else "single GPU",
             "graph": not a.no_graph,
+            "launches_per_layer": [[name, N, K, ab] for (name, N, K, ab) in launch_lins],
         },
         "roofline": {
             "kernel": "fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else "fq_gemm_decode_kernel (+ quantize where unfused)",

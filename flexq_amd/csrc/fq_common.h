@@ -79,7 +79,11 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
         mx = fmaxf(mx, fabsf(v[i]));
     }
     mx = max16(mx);
-    const float maxv = mx / (float)hi;  // IEEE fp32 division (no fast-math in this build)
+    // IEEE fp32 absmax / hi as a Newton-corrected product with y = RN(1/hi): bit-identical over
+    // every fp16 absmax (exhaustive: tests/test_oracle.py::test_quantizer_division_by_constant_is_exact)
+    const float fhi = (float)hi, y = bits == 8 ? (float)(1.0 / 127.0) : (float)(1.0 / 31.0);
+    const float m1 = mx * y;
+    const float maxv = __builtin_isfinite(m1) ? fmaf(fmaf(-m1, fhi, mx), y, m1) : m1;
     const uint16_t sh = f2h(maxv);
     const float r = h2f(sh);
     const float rc = __builtin_amdgcn_rcpf(r);

@@ -221,18 +221,28 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
                                              LDS_PTR(xh_st + c * 256), 16, 0, 0);
         }
     };
-    auto x_quant = [&](int r0) {
-        for (int c = 0; c < xwin && r0 + c < R; c += 4) {  // wave-uniform bounds
+    auto x_store = [&](int rg, uint2 codes, uint16_t sh) {
+        if (rg < R) {
+            const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+            ds_write_b64(lds_addr(x_st + rg * 128 + xswz(row, qsub >> 1) + (qsub & 1) * 8), codes);
+            if (qsub == 0) ds_write_b32(lds_addr(xs_st + (j * XSR + row) * 4), sh);
+        }
+    };
+    auto x_quant = [&](int r0) {  // two 4-pair chunks per step where possible (chains interleave)
+        for (int c = 0; c < xwin && r0 + c < R; c += 8) {  // wave-uniform bounds
             const int rg = r0 + c + (lane >> 4);
-            const v4i raw = ds_read_b128(lds_addr(xh_st + c * 256 + lane * 16));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);  // no use of `raw` may move above the wait
-            uint2 codes;
-            const uint16_t sh = quant_group16(make_uint4(raw[0], raw[1], raw[2], raw[3]), abits, codes);
-            if (rg < R) {
-                const int j = M == 1 ? rg : rg / M, row = rg - j * M;
-                ds_write_b64(lds_addr(x_st + rg * 128 + xswz(row, qsub >> 1) + (qsub & 1) * 8), codes);
-                if (qsub == 0) ds_write_b32(lds_addr(xs_st + (j * XSR + row) * 4), sh);
+            const bool two = c + 4 < xwin && r0 + c + 4 < R;
+            v4i raw0 = ds_read_b128(lds_addr(xh_st + c * 256 + lane * 16));
+            v4i raw1 = ds_read_b128(lds_addr(xh_st + (two ? c + 4 : c) * 256 + lane * 16));
+            // the wait redefines raw0/raw1, so no use of them can be placed above it
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(raw0), "+v"(raw1)::"memory");
+            uint2 codes0;
+            const uint16_t sh0 = quant_group16(make_uint4(raw0[0], raw0[1], raw0[2], raw0[3]), abits, codes0);
+            x_store(rg, codes0, sh0);
+            if (two) {
+                uint2 codes1;
+                const uint16_t sh1 = quant_group16(make_uint4(raw1[0], raw1[1], raw1[2], raw1[3]), abits, codes1);
+                x_store(rg + 4, codes1, sh1);
             }
         }
     };

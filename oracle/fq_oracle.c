@@ -363,3 +363,28 @@ int fqo_unpack_fq6(const uint8_t *packed, int N, int K, int8_t *wq, uint16_t *ws
                 }
     return 0;
 }
+
+/* ------------------------------------------------------------- quantizer arithmetic checks */
+/* The HIP quantizer computes maxv = absmax / hi as a Newton-corrected product with the
+ * correctly rounded constant y = RN(1/hi) (flexq_amd/csrc/fq_common.h quant_group16):
+ *   q1 = RN(a * y);  r = fma(-q1, hi, a);  q = isfinite(q1) ? fma(r, y, q1) : q1.
+ * Returns how many of the 65536 fp16 bit patterns a (as float, |a|), plus the absmax seed -1,
+ * give q != RN(a / hi) (bitwise; NaN compares equal to NaN).  Test infrastructure only. */
+long fqo_check_div_by_const(int hi) {
+    const float fhi = (float)hi;
+    const float y = (float)(1.0 / (double)hi);
+    long bad = 0;
+    for (int u = 0; u <= 65536; u++) {
+        float a = u < 65536 ? fabsf(fqo_f16_to_f32((uint16_t)u)) : -1.0f;
+        volatile float ref = a / fhi;
+        float q1 = a * y;
+        float r = fmaf(-q1, fhi, a);
+        float q = isfinite(q1) ? fmaf(r, y, q1) : q1;
+        if (isnan(ref) && isnan(q)) continue;
+        uint32_t b0, b1;
+        memcpy(&b0, (const void *)&ref, 4);
+        memcpy(&b1, &q, 4);
+        if (b0 != b1) bad++;
+    }
+    return bad;
+}

@@ -134,6 +134,15 @@ def gemm(xq, xs, wq, ws, want_acc=False):
     return out, acc, mag
 
 
+def check_div_by_const(hi):
+    """Mismatches of the quantizer's Newton-corrected absmax / hi against IEEE division over
+    every fp16 absmax (oracle/fq_oracle.c fqo_check_div_by_const); 0 means bit-identical."""
+    f = lib().fqo_check_div_by_const
+    f.argtypes = [ctypes.c_int]
+    f.restype = ctypes.c_long
+    return int(f(hi))
+
+
 def fq6_bytes(N, K):
     return int(lib().fqo_fq6_bytes(N, K))
 

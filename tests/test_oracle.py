@@ -199,3 +199,10 @@ def test_f16_conversion_rounding():
     vals = rng(1).standard_normal(100000).astype(np.float32) * 100
     got = np.array([L.fqo_f32_to_f16(float(v)) for v in vals[:5000]], dtype=np.uint16)
     np.testing.assert_array_equal(got, vals[:5000].astype(np.float16).view(np.uint16))
+
+
+@pytest.mark.parametrize("hi", [31, 127])
+def test_quantizer_division_by_constant_is_exact(hi):
+    """The device quantizer replaces absmax / (2^(b-1)-1) by a Newton-corrected product with the
+    rounded reciprocal constant; over every fp16 absmax it is bit-identical to IEEE division."""
+    assert oracle.check_div_by_const(hi) == 0
