@@ -165,6 +165,18 @@ def fp16_compare(shapes, M, abits, dev, reps=20):
     return out
 
 
+def pmc_traffic(config, merge):
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 FETCH_SIZE
+    pass for this workload (profiles/rNN_pmc_summary.json, written by tools/pmc_summary.py, with
+    the gfx950 x2 correction applied).  None when no pass matches."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), reverse=True):
+        d = json.load(open(path))
+        if d.get("config") == config and d.get("merged_gate_up", False) == merge:
+            return d["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(budget_s=15.0):
     """The reference's CPU fake-quant QuantLinear forward (oracle restatement, torch CPU ops) on a
     bounded sample: LLaMA-2-7B linear shapes at M=1, fp16, weights re-fake-quantised every forward
@@ -283,6 +295,7 @@ def main():
                                 for (_, N, K, ab) in launch_lins) / launches
     achieved = bytes_launch / per_launch_s / 1e9
     del g2
+    traffic, traffic_src = pmc_traffic(a.config, merge) if world == 1 else (None, None)
 
     res = {
         "metric": "W6A6 GEMM TFLOPS-equiv + tok/s on LLaMA-2-7B linear shapes, 1/2/4/8 GPU",
@@ -313,7 +326,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_over_alg": round(traffic / bytes_launch, 4) if traffic else None,
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
             "fused_launches": all(fused.values()),
