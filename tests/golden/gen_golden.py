@@ -98,6 +98,31 @@ def main():
                 e[f"{name}_a{bits}_codes"] = codes.to(torch.int8).numpy()
                 e[f"{name}_a{bits}_xhat"] = xhat.numpy()
         np.savez_compressed(os.path.join(HERE, f"edge_{dname}.npz"), **e)
+
+        # other quantizer configurations of the operator surface (main.py:222-296 without
+        # --symmetric, per-token activations, symmetric with a zero point, fix0to1)
+        v = {}
+        x = torch.from_numpy(act_input(8, 512, seed=31)).to(dt)
+        for tag, params in (
+                ("asym_g128_a6", dict(n_bits=6, symmetric=False, dynamic_method="per_group", group_size=128)),
+                ("asym_g128_a8", dict(n_bits=8, symmetric=False, dynamic_method="per_group", group_size=128)),
+                ("asym_tok_a8", dict(n_bits=8, symmetric=False, dynamic_method="per_token")),
+                ("asym_g128_a2", dict(n_bits=2, symmetric=False, dynamic_method="per_group", group_size=128)),
+                ("symzp_g128_a6", dict(n_bits=6, symmetric=True, dynamic_method="per_group", group_size=128)),
+                ("sym_tok_a6", dict(n_bits=6, symmetric=True, dynamic_method="per_token", disable_zero_point=True)),
+                ("a16", dict(n_bits=16, symmetric=False, dynamic_method="per_group", group_size=128))):
+            q = UniformAffineQuantizer(**params)
+            with torch.no_grad():
+                v[f"{tag}_xhat"] = q(x.clone()).numpy()
+            if q.scale is not None:
+                v[f"{tag}_scale"] = q.scale.numpy()
+            if q.round_zero_point is not None:
+                v[f"{tag}_zero"] = q.round_zero_point.numpy()
+        p01 = torch.from_numpy(np.abs(act_input(4, 256, seed=5)) / 8).to(dt).clamp(0, 1)
+        q = UniformAffineQuantizer(n_bits=8, metric="fix0to1")
+        with torch.no_grad():
+            v["fix0to1_a8_xhat"] = q(p01.clone()).numpy()
+        np.savez_compressed(os.path.join(HERE, f"variants_{dname}.npz"), **v)
     print("golden vectors written to", HERE)
 
 
