@@ -67,16 +67,17 @@ __device__ __forceinline__ int cvt_i32_sat(float v) {
     return r;
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &codes) {
-    const uint16_t h[8] = {(uint16_t)raw.x, (uint16_t)(raw.x >> 16), (uint16_t)raw.y, (uint16_t)(raw.y >> 16),
-                           (uint16_t)raw.z, (uint16_t)(raw.z >> 16), (uint16_t)raw.w, (uint16_t)(raw.w >> 16)};
+    const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
     const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
-    float v[8];
+    v2f v[4];
     float mx = -1.0f;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        v[i] = h2f(h[i]);
-        mx = fmaxf(mx, fabsf(v[i]));
+    for (int i = 0; i < 4; i++) {
+        v[i] = v2f{h2f((uint16_t)wd[i]), h2f((uint16_t)(wd[i] >> 16))};
+        mx = fmaxf(mx, fmaxf(fabsf(v[i].x), fabsf(v[i].y)));
     }
     mx = max16(mx);
     // IEEE fp32 absmax / hi as a Newton-corrected product with y = RN(1/hi): bit-identical over
@@ -87,18 +88,26 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
     const uint16_t sh = f2h(maxv);
     const float r = h2f(sh);
     const float rc = __builtin_amdgcn_rcpf(r);
-    const bool newton = __builtin_isfinite(r) && r != 0.0f;  // else the plain product (inf/NaN class)
+    const v2f r2 = {r, r}, rc2 = {rc, rc};
+    // Newton step unless the scale is 0 / inf (then the plain product has the IEEE quotient's
+    // value class); wave-uniform in practice, so the common case carries no select.
+    const bool newton = __builtin_isfinite(r) && r != 0.0f;
+    v2f q[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {  // packed fp32 math: v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32
+        const v2f q1 = v[i] * rc2;
+        q[i] = q1;
+        if (newton) q[i] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, r2, v[i]), rc2, q1);
+    }
     uint32_t w[2] = {0, 0};
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const float q1 = v[i] * rc;
-        const float q = newton ? fmaf(fmaf(-q1, r, v[i]), rc, q1) : q1;
+    for (int i = 0; i < 4; i++) {
         // roundf = trunc(q + copysign(0.5, q)) here: q is either an exact half-integer or at
         // least 2^-12 (relative) away from one, so the addition cannot cross an integer; the
-        // saturating conversion then maps +-inf to the int range and NaN to 0 (sat_clamp).
-        const int c = cvt_i32_sat(__builtin_truncf(q + __builtin_copysignf(0.5f, q)));
-        const int qc = min(max(c, lo), hi);  // v_med3_i32
-        w[i >> 2] |= (uint32_t)(qc & 255) << (8 * (i & 3));
+        // truncating, saturating v_cvt_i32_f32 then also maps +-inf to the int range, NaN to 0.
+        const v2f t = q[i] + v2f{__builtin_copysignf(0.5f, q[i].x), __builtin_copysignf(0.5f, q[i].y)};
+        const int c0 = min(max(cvt_i32_sat(t.x), lo), hi), c1 = min(max(cvt_i32_sat(t.y), lo), hi);
+        w[i >> 1] |= ((uint32_t)(c0 & 255) | ((uint32_t)(c1 & 255) << 8)) << (16 * (i & 1));
     }
     codes = make_uint2(w[0], w[1]);
     return sh;

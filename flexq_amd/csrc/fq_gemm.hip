@@ -316,6 +316,10 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
         FQ_STAMP(5);
         x_quant(0);
         FQ_STAMP(6);
+        if (ABL & 32) {  // development: the same code once more (instruction cache now warm);
+            if (!(ABL & 64)) x_quant(0);  // with 64: nothing, i.e. the cost of a stamp itself
+            FQ_STAMP(4);
+        }
         for (int r0 = xwin; r0 < R; r0 += xwin) {  // M > 4 or long K: later windows
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous window was read
             x_fetch(r0);
@@ -783,7 +787,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
-        FQ_ABL(2) FQ_ABL(4) FQ_ABL(6) FQ_ABL(8) FQ_ABL(14) FQ_ABL(16)
+        FQ_ABL(2) FQ_ABL(4) FQ_ABL(6) FQ_ABL(8) FQ_ABL(14) FQ_ABL(16) FQ_ABL(48) FQ_ABL(112)
 #undef FQ_ABL
     }
 #endif

@@ -23,7 +23,7 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     R, COPIES = 20, 6
-    os.environ["FQ_DEV_ABLATION"] = "16"
+    os.environ["FQ_DEV_ABLATION"] = os.environ.get("FQ_STAMP_MASK", "16")
     L = _lib.load()
     L.fq_dev_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     stream = torch.cuda.Stream()
@@ -74,7 +74,9 @@ def main():
                   f"stage={us(np.median(st[:, 7] - st[:, 0])):5.2f} issue={us(np.median(st[:, 1] - st[:, 0])):5.2f} first={us(np.median(st[:, 2] - st[:, 1])):5.2f} "
                   f"loop={us(np.median(st[:, 3] - st[:, 2])):6.2f} (max {us((st[:, 3] - st[:, 2]).max()):6.2f}) "
                   f"end_spread={us(end.max() - end.min()):5.2f} fixup={us(np.median(np.maximum(st[:, 4] - st[:, 3], 0))):5.2f}"
-                  + (f" xwait={us(np.median(st[:, 5] - st[:, 1])):5.2f} quant={us(np.median(st[:, 6] - st[:, 5])):5.2f}" if linear else ""),
+                  + (f" xwait={us(np.median(st[:, 5] - st[:, 1])):5.2f} quant={us(np.median(st[:, 6] - st[:, 5])):5.2f}"
+                     + (f" quant2={us(np.median(st[:, 4] - st[:, 6])):5.2f}" if os.environ.get("FQ_STAMP_MASK") in ("48", "112") else "")
+                     if linear else ""),
                   flush=True)
             del copies, graph
 
