@@ -657,6 +657,7 @@ __global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
 // =============================================================================================
 struct DecodePlan {
     int MT, S, grid, IPW, RC, XS, SS, xwin;  // xwin: fused fp16 window (0 = not fused)
+    int cost4;                               // modelled time, quarter-blocks per wave (see decode_plan)
     bool fits;
 };
 static const size_t kLdsMax = 160 * 1024;
@@ -680,6 +681,14 @@ static size_t decode_lds_bytes(const DecodePlan &p, int M, int N, int K) {
            (size_t)p.RC * NW * M * 16 * 4 + 4 * (size_t)p.IPW + 16;
 }
 
+// Cost model, in quarter-blocks of one wave's stream (one 1.5 KiB block per wave at the
+// whole-chip rate is ~0.7 us for the 7B shapes; tools/fuse_bench.py, tools/stamps.py):
+//   stream   4 x items per WG x groups per wave
+//   k-split  12 (fix-up round trip, 1.1-1.7 us) + the slab bytes each WG writes and reads
+//   fused    1 per (group, row) pair a wave quantizes (~0.17 us each, measured M = 1..16)
+//   split    12 for the separate quantize launch (~2.2 us incl. its launch)
+static const int kSplitQuantCost4 = 12;
+
 // fused: only the fully staged variant (the quantizer writes straight into the staged regions);
 // `fits` is false when that does not fit LDS and the caller must quantize separately.
 static DecodePlan decode_plan(int M, int N, int K, bool fused) {
@@ -688,10 +697,9 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused) {
     const int NT = (N + 15) / 16, G = K / FQ_GROUP;
     const int cus = device_cus();
     const int NW = decode_waves(p.MT);
-    // k-split S: minimise the largest per-wave block count (items per WG x groups per wave),
-    // +3 for the fix-up of S > 1 (measured 1.1-1.7 us, tools/stamps.py: ~3 blocks per wave at
-    // the whole-chip streaming rate).  S divides the grid so that z = blockIdx % S is fixed per
-    // WG; ties keep the smaller S.
+    // k-split S minimises the modelled GEMM cost; S divides the grid so that z = blockIdx % S is
+    // fixed per WG; ties keep the smaller S.  S (hence the summation order) is the same fused or
+    // not, so fq_linear_w6ax gives the same bits whichever way it runs.
     long best = -1;
     p.S = 1;
     for (int S = 1; S <= G && S <= cus; S++) {
@@ -699,13 +707,16 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused) {
         const int grid = items < cus ? items : cus;
         if (grid % S) continue;
         const long ipw = (items + grid - 1) / grid;
-        const long gz = (G + S - 1) / S;
-        const long cost = ipw * ((gz + NW - 1) / NW) + (S > 1 ? 3 : 0);
+        const long ngw = ((G + S - 1) / S + NW - 1) / NW;
+        long cost = 4 * ipw * ngw;
+        if (S > 1) cost += 12 + 4 * ipw * M * 128 / (NW * FQ_BLOCK);
         if (best < 0 || cost < best) {
             best = cost;
             p.S = S;
         }
     }
+    const int ngw = ((G + p.S - 1) / p.S + NW - 1) / NW;
+    p.cost4 = (int)best + (fused ? ngw * M : kSplitQuantCost4);
     const int items = NT * p.S;
     p.grid = items < cus ? items : cus;
     p.IPW = (items + p.grid - 1) / p.grid;
@@ -734,10 +745,10 @@ static const size_t kTicketBytes = 256 * 1024;  // tickets for up to 65536 16-co
 extern "C" size_t fq_gemm_workspace_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
     if (M > 32) return 0;
-    DecodePlan p = decode_plan(M, N, K, false);  // S does not depend on the staging variant
-    if (p.S == 1) return 0;
+    const int S = decode_plan(M, N, K, false).S;  // the same for every staging variant and fused
+    if (S == 1) return 0;
     const size_t Npad = (size_t)((N + 15) / 16) * 16;
-    return kTicketBytes + (size_t)p.S * M * Npad * sizeof(float);
+    return kTicketBytes + (size_t)S * M * Npad * sizeof(float);
 }
 
 extern "C" fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_t stream) {
@@ -817,9 +828,19 @@ static fq_status dispatch_decode(const DecodePlan &p, const DecodeArgs &a, hipSt
     }
 }
 
+// The fused one-launch linear is taken when it fits and its modelled cost (in-kernel quantizer
+// redundant across WGs) does not exceed the split plan's (quantize launch + GEMM).
+static bool decode_fuse(int M, int N, int K, DecodePlan *out) {
+    if (M > 32) return false;
+    const DecodePlan f = decode_plan(M, N, K, true);
+    if (!f.fits || f.cost4 > decode_plan(M, N, K, false).cost4) return false;
+    if (out) *out = f;
+    return true;
+}
+
 extern "C" size_t fq_linear_act_scratch_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
-    if (M <= 32 && decode_plan(M, N, K, true).fits) return 0;
+    if (decode_fuse(M, N, K, nullptr)) return 0;
     return (size_t)M * K + (size_t)M * (K / FQ_GROUP) * 2;
 }
 
@@ -828,9 +849,8 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
                                  uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
                                  hipStream_t s, bool *launched) {
     *launched = false;
-    if (M > 32) return FQ_OK;
-    DecodePlan p = decode_plan(M, N, K, true);
-    if (!p.fits) return FQ_OK;
+    DecodePlan p;
+    if (!decode_fuse(M, N, K, &p)) return FQ_OK;
     const size_t need = fq_gemm_workspace_bytes(M, N, K);
     if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
     DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace};

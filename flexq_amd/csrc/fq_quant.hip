@@ -1,6 +1,8 @@
 // fq_quant.hip -- dynamic activation quantizer, fq6 weight packer and the reference-layout
 // converters for gfx950.  HBM-bound byte work: 16-byte-per-lane coalesced loads, 16-lane
 // (one DPP row) max-reductions, no LDS round trips.
+#include <type_traits>
+
 #include "fq_common.h"
 
 // =============================================================================================
@@ -14,25 +16,28 @@
 //   MODE 0: xq int8 [M][K] + xs fp16 [K/128][M]          (this build's GEMM input)
 //   MODE 1: reference bit planes [K/128][M/c][b][c][4] + duplicated x_scale (drop-in pack)
 // =============================================================================================
-template <int MODE>
+// IDX: index type -- 32-bit when M*K fits (64-bit division alone costs ~100 instructions per
+// lane, comparable to the quantizer itself), 64-bit otherwise.
+template <int MODE, typename IDX>
 __global__ __launch_bounds__(256) void fq_quantize_act_kernel(
     const uint16_t *__restrict__ x, int M, int K, int bits, int8_t *__restrict__ xq,
     uint16_t *__restrict__ xs, int32_t *__restrict__ planes, uint16_t *__restrict__ xs_dup) {
+    using U = typename std::conditional<sizeof(IDX) == 4, unsigned, unsigned long>::type;
     const int G = K / FQ_GROUP;
-    const long T = (long)M * G;  // total groups
+    const IDX T = (IDX)M * G;  // total groups
     const int lane = threadIdx.x & 63;
     const int sub = lane & 15;  // position inside the group
-    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    const IDX wave = (IDX)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const IDX nwaves = (IDX)((gridDim.x * blockDim.x) >> 6);
 
-    for (long chunk = wave; chunk * 4 < T; chunk += nwaves) {
-        const long gi = chunk * 4 + (lane >> 4);  // flat group index of this lane
+    for (IDX chunk = wave; chunk * 4 < T; chunk += nwaves) {
+        const IDX gi = chunk * 4 + (lane >> 4);  // flat group index of this lane
         const bool valid = gi < T;
         uint4 raw = make_uint4(0, 0, 0, 0);
         if (valid) raw = *reinterpret_cast<const uint4 *>(x + gi * FQ_GROUP + sub * 8);
         uint2 codes;
         const uint16_t sh = quant_group16(raw, bits, codes);
-        const long m = gi / G, g = gi - (gi / G) * G;
+        const IDX m = (IDX)((U)gi / (U)G), g = gi - m * G;
         if (MODE == 0) {
             if (valid) {
                 *reinterpret_cast<uint2 *>(xq + gi * FQ_GROUP + sub * 8) = codes;
@@ -78,8 +83,12 @@ extern "C" fq_status fq_quantize_act(const uint16_t *x, int M, int K, int abits,
     if (M <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     const long groups = (long)M * (K / FQ_GROUP);
-    hipLaunchKernelGGL(fq_quantize_act_kernel<0>, dim3(quant_grid(groups)), dim3(256), 0,
-                       (hipStream_t)stream, x, M, K, abits, xq, xs, nullptr, nullptr);
+    if (groups * FQ_GROUP < (1L << 31))
+        hipLaunchKernelGGL((fq_quantize_act_kernel<0, int>), dim3(quant_grid(groups)), dim3(256), 0,
+                           (hipStream_t)stream, x, M, K, abits, xq, xs, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL((fq_quantize_act_kernel<0, long>), dim3(quant_grid(groups)), dim3(256), 0,
+                           (hipStream_t)stream, x, M, K, abits, xq, xs, nullptr, nullptr);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
@@ -91,7 +100,7 @@ extern "C" fq_status fq_ref_quantize_bit_packing(const uint16_t *x, int32_t *pac
     if (M <= 0 || K <= 0 || K % FQ_GROUP || (M > 8 && M % 8)) return FQ_ERR_SHAPE;
     if (bits != 6 && bits != 8) return FQ_ERR_BITS;
     const long groups = (long)M * (K / FQ_GROUP);
-    hipLaunchKernelGGL(fq_quantize_act_kernel<1>, dim3(quant_grid(groups)), dim3(256), 0,
+    hipLaunchKernelGGL((fq_quantize_act_kernel<1, long>), dim3(quant_grid(groups)), dim3(256), 0,
                        (hipStream_t)stream, x, M, K, bits, nullptr, nullptr, packed, x_scale_dup);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
