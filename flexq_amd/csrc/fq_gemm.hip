@@ -43,6 +43,26 @@ __device__ __forceinline__ uint32_t ds_read_u16(uint32_t a) {
     return v;
 }
 
+// immediate-offset forms (offset < 64 KiB folded into the instruction)
+template <int OFF>
+__device__ __forceinline__ v4i ds_read_b128_at(uint32_t a) {
+    v4i v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+}
+template <int OFF>
+__device__ __forceinline__ v2u ds_read_b64_at(uint32_t a) {
+    v2u v;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t ds_read_u16_at(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_u16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+}
+
 template <int U, int D>
 __device__ __forceinline__ void wait_ring(int later) {
     // s_waitcnt takes an immediate: `later` (< D) blocks of U DMA instructions may stay in flight
@@ -482,89 +502,105 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
 }
 
 // =============================================================================================
-// Prefill kernel (M > 32): MFMA-bound.  Block tile 128 x 128, 4 waves as 2 (M) x 2 (N), each
-// wave 64 x 64 = 4 x 4 tiles of 16x16.  Per 128-wide group the block stages
-//   A: 128 rows x 128 B int8, 16-byte chunks XOR-swizzled by (row & 7) (xswz) so each 8-lane
+// Prefill kernel (M > 32): int8-MFMA bound.  WG tile 256 (M) x 128 (N), 8 waves as 4 (M) x 2 (N),
+// each wave 64 x 64 = 4 x 4 tiles of 16x16; one k-step per 128-wide group.  Per group a stage holds
+//   A  256 rows x 128 B int8, 16-byte chunks XOR-swizzled by (row & 7) (xswz), so each 8-lane
 //      phase of a ds_read_b128 hits 8 distinct bank groups;
-//   B: 8 n-tiles x 1.5 KiB packed weights, a straight copy of the fq6 blocks (3 planes x 64
-//      lanes x 8 B), read back as three ds_read_b64 per n-tile and group;
-//   the 128 x-scales and 128 w-scales of the group,
-// in registers one group ahead (global loads issued before the MFMAs, LDS writes after), with
-// two LDS buffers.  Group accumulators are int32; dequant is fp32 FMA per group.
+//   B  the 8 fq6 blocks of the WG's 16-column tiles, verbatim (3 planes x 64 lanes x 8 B), read
+//      back as three ds_read_b64 per tile;
+//   the 256 x-scales (one per dword) and 128 w-scales of the group.
+// Staging is LDS-DMA only (global_load_lds: no VGPR round trip, no ds_write pass); three stages,
+// two in flight across the one raw barrier per group (counted vmcnt, never vmcnt(0) in the loop:
+// cdna_hip_programming.md "Pipelining across barriers").  Each wave issues PF_DMA DMA
+// instructions per stage: 4 of A (32 rows), 2 of B (waves 0-5) or of x-scales (waves 6-7), and
+// the w-scales (wave 7) or a filler.  Group accumulators are int32; dequant is one fp16 scale product and
+// one fp32 FMA per element and group, in the reference's order.
 // =============================================================================================
-constexpr int PF_BM = 128, PF_BN = 128;
-constexpr int PF_A_BYTES = PF_BM * FQ_GROUP;                // 16 KiB
-constexpr int PF_B_BYTES = (PF_BN / 16) * FQ_BLOCK;         // 12 KiB
-constexpr int PF_STAGE = PF_A_BYTES + PF_B_BYTES + 2 * PF_BM * 2 + 2 * PF_BN * 2;  // + xs, ws (x2 spare)
-
-struct PrefillStage {
-    uint4 a[4];
-    uint4 b[3];
-    uint16_t xsv, wsv;
-};
-
-__device__ __forceinline__ void prefill_gload(PrefillStage &st, const int8_t *__restrict__ xq,
-                                              const uint16_t *__restrict__ xs,
-                                              const uint32_t *__restrict__ wpk,
-                                              const uint16_t *__restrict__ wsb, int M, int N, int K,
-                                              int G, int m0, int t0, int NT, int g, int tid) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int c = tid + 256 * j;  // 1024 chunks of 16 B
-        const int row = c >> 3, cc = c & 7;
-        const int m = m0 + row;
-        if (m < M) st.a[j] = *reinterpret_cast<const uint4 *>(xq + (long)m * K + g * FQ_GROUP + cc * 16);
-        else st.a[j] = make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int c = tid + 256 * j;  // 768 chunks of 16 B = 8 n-tiles x 1.5 KiB
-        const int nt = c / 96, within = c - nt * 96;
-        const int t = t0 + nt;
-        if (t < NT) st.b[j] = reinterpret_cast<const uint4 *>(wpk + (long)(t * G + g) * (FQ_BLOCK / 4))[within];
-        else st.b[j] = make_uint4(0, 0, 0, 0);
-    }
-    st.xsv = 0;
-    st.wsv = 0;
-    if (tid < PF_BM) {
-        const int m = m0 + tid;
-        if (m < M) st.xsv = xs[(long)g * M + m];
-    } else {
-        const int c = tid - PF_BM, t = t0 + c / 16;  // blocked scales, pad columns hold 0
-        if (t < NT) st.wsv = wsb[((long)t * G + g) * 16 + (c & 15)];
-    }
-}
-
-__device__ __forceinline__ void prefill_swrite(const PrefillStage &st, char *buf, int tid) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int c = tid + 256 * j;
-        *reinterpret_cast<uint4 *>(buf + (c >> 3) * 128 + xswz(c >> 3, c & 7)) = st.a[j];
-    }
-    char *bb = buf + PF_A_BYTES;
-#pragma unroll
-    for (int j = 0; j < 3; j++) *reinterpret_cast<uint4 *>(bb + (tid + 256 * j) * 16) = st.b[j];
-    uint16_t *sc = reinterpret_cast<uint16_t *>(buf + PF_A_BYTES + PF_B_BYTES);
-    sc[tid] = (tid < PF_BM) ? st.xsv : st.wsv;  // [0,128) x-scales, [128,256) w-scales
-}
+constexpr int PF_BM = 256, PF_BN = 128, PF_TILES = PF_BN / 16;
+constexpr int PF_A_BYTES = PF_BM * FQ_GROUP;              // 32 KiB
+constexpr int PF_B_OFF = PF_A_BYTES;
+constexpr int PF_XS_OFF = PF_B_OFF + PF_TILES * FQ_BLOCK;  // + 12 KiB
+constexpr int PF_WS_OFF = PF_XS_OFF + PF_BM * 4;           // x-scales one per dword
+constexpr int PF_PAD_OFF = PF_WS_OFF + PF_BN * 2;          // filler DMA target (never read)
+constexpr int PF_STAGE = PF_PAD_OFF + 16;                  // 46352 B
+constexpr int PF_DEPTH = 3;                                // 139056 B of LDS: one WG per CU
+constexpr int PF_DMA = 7;                                  // DMA instructions per wave and stage
+// s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
+constexpr int vmcnt_only(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
 template <bool DBG>
-__global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
+__global__ __launch_bounds__(512, 1) void fq_gemm_prefill_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
     int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ __attribute__((aligned(16))) char sb0[PF_STAGE], sb1[PF_STAGE], sb2[PF_STAGE];
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wid >> 1, wn = wid & 1;
 
-    // XCD-aware block order: consecutive logical tiles on one XCD share A rows through its L2.
-    const int nbx = gridDim.x, nby = gridDim.y, nwg = nbx * nby;
-    const int bid = blockIdx.y * nbx + blockIdx.x;
-    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    // Block order: the bijective XCD remap (consecutive logical tiles run on one XCD), then groups
+    // of 8 M-panels walked M-fastest, so the WGs resident on an XCD share A and B k-slices in L2.
+    const int nbm = (M + PF_BM - 1) / PF_BM, nbn = (NT + PF_TILES - 1) / PF_TILES, nwg = nbm * nbn;
+    const int bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
     const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
-    const int bn = lid % nby, bm = lid / nby;  // N fastest: blocks sharing an A panel are adjacent
-    const int m0 = bm * PF_BM, t0 = bn * (PF_BN / 16);
+    const int span = 8 * nbn, first = (lid / span) * 8;
+    const int gsz = nbm - first < 8 ? nbm - first : 8;
+    const int bm = first + (lid % span) % gsz, bn = (lid % span) / gsz;
+    const int m0 = bm * PF_BM, t0 = bn * PF_TILES;
+
+    // ---- per-lane DMA sources at group 0 (a group adds 128 B to A, 1536 B to B, M or 16 to scales)
+    const int8_t *asrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int row = 32 * wid + 8 * i + (lane >> 3);
+        const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M are computed, never stored
+        asrc[i] = xq + (size_t)m * K + ((lane & 7) ^ (row & 7)) * 16;
+    }
+    const char *bsrc[2] = {nullptr, nullptr};
+    const uint16_t *ssrc[2] = {nullptr, nullptr};
+    if (wid < 6) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int o = (2 * wid + i) * 1024 + lane * 16;  // byte of the stage's B image
+            const int nt = o / FQ_BLOCK, t = t0 + nt < NT ? t0 + nt : NT - 1;
+            bsrc[i] = reinterpret_cast<const char *>(wpk) + (size_t)t * G * FQ_BLOCK + (o - nt * FQ_BLOCK);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int row = 128 * (wid - 6) + 64 * i + lane;
+            ssrc[i] = xs + (m0 + row < M ? m0 + row : M - 1);
+        }
+    }
+    const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;
+    const uint16_t *wsrc = wsb + (size_t)wt * G * 16 + 8 * (lane & 1);
+
+    // LDS read offsets of the wave's A rows (xswz: row & 7 == lane & 7 for every 16-row tile) and
+    // of its 4 x-scales per tile
+    const int arow = wm * 64 + (lane & 15);
+    const uint32_t a_off[2] = {(uint32_t)(arow * FQ_GROUP + xswz(arow, lane >> 4)),
+                               (uint32_t)(arow * FQ_GROUP + xswz(arow, 4 + (lane >> 4)))};
+    const uint32_t x_off = PF_XS_OFF + (wm * 64 + 4 * (lane >> 4)) * 4;
+
+    auto stage = [&](int g, char *buf) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds(asrc[i] + g * FQ_GROUP, LDS_PTR(buf + (32 * wid + 8 * i) * FQ_GROUP), 16, 0, 0);
+        if (wid < 6) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds(bsrc[i] + (size_t)g * FQ_BLOCK, LDS_PTR(buf + PF_B_OFF + (2 * wid + i) * 1024), 16, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                __builtin_amdgcn_global_load_lds(ssrc[i] + (size_t)g * M, LDS_PTR(buf + PF_XS_OFF + (128 * (wid - 6) + 64 * i) * 4), 2, 0, 0);
+        }
+        // the w-scales (wave 7, 16 lanes), or one 4-byte filler DMA into the pad word, so that every
+        // wave issues the same PF_DMA instructions per stage and one counted wait serves all paths
+        if (lane < (wid == 7 ? 16 : 1))
+            __builtin_amdgcn_global_load_lds(wsrc + (wid == 7 ? g * 16 : 0), LDS_PTR(buf + (wid == 7 ? PF_WS_OFF : PF_PAD_OFF)), 16, 0, 0);
+    };
 
     float out[4][4][4];
 #pragma unroll
@@ -574,80 +610,108 @@ __global__ __launch_bounds__(256, 2) void fq_gemm_prefill_kernel(
 #pragma unroll
             for (int r = 0; r < 4; r++) out[i][j][r] = 0.f;
 
-    PrefillStage st;
-    prefill_gload(st, xq, xs, wpk, wsb, M, N, K, G, m0, t0, NT, 0, tid);
-    prefill_swrite(st, smem, tid);
-    __syncthreads();
+    // One k-step: wait for stage g, barrier, refill the buffer stage g - 1 used with stage g + 2,
+    // compute on stage g.  The loop is unrolled by the stage count so that every buffer is a
+    // distinct __shared__ object: the compiler's wait insertion then sees that the ds_reads of
+    // stage g cannot alias the DMA still landing in the other two buffers (with one array it
+    // emits vmcnt(0) before the first ds_read of every k-step and drains the pipeline).
+    auto kstep = [&](int g, const char *buf, char *refill) {
+        // stage g landed for every wave (own count, then the barrier), and every wave is done
+        // reading stage g - 1, whose buffer the DMA below refills
+        // (the builtin, not inline asm: the compiler's own wait insertion accounts for it)
+        // Every step issues one stage (past the last group: a copy of it into a buffer no step reads
+        // again), so the same count holds on every path: stage g + 1 may stay in flight.
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_DMA));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        stage(g + 2 < G ? g + 2 : G - 1, refill);
 
-    for (int g = 0; g < G; g++) {
-        char *buf = smem + (g & 1) * PF_STAGE;
-        if (g + 1 < G) prefill_gload(st, xq, xs, wpk, wsb, M, N, K, G, m0, t0, NT, g + 1, tid);
-
+        // LDS reads are inline asm (the compiler's wait insertion cannot tell them from the DMA
+        // landing in the other buffers and would drain it with vmcnt(0)); their lgkmcnt waits are
+        // counted here and re-define the loaded registers, so no use can move above its wait.
+        // Issue order: B planes + w-scales (16), then A + x-scales per 16-row tile (4 x 3).
+        const uint32_t lb = lds_addr(buf);
+        const uint32_t bb = lb + wn * 4 * FQ_BLOCK + lane * 8;
+        const uint32_t wb = lb + (wn * 64 + (lane & 15)) * 2;
+        const uint32_t ab0 = lb + a_off[0], ab1 = lb + a_off[1], xb = lb + x_off;
+        v2u pl[4][3];
+        uint32_t wv[4];
+#define FQ_PF_B(ni)                                                      \
+        pl[ni][0] = ds_read_b64_at<PF_B_OFF + (ni) * FQ_BLOCK>(bb);       \
+        pl[ni][1] = ds_read_b64_at<PF_B_OFF + (ni) * FQ_BLOCK + 512>(bb); \
+        pl[ni][2] = ds_read_b64_at<PF_B_OFF + (ni) * FQ_BLOCK + 1024>(bb); \
+        wv[ni] = ds_read_u16_at<PF_WS_OFF + (ni) * 32>(wb);
+        FQ_PF_B(0) FQ_PF_B(1) FQ_PF_B(2) FQ_PF_B(3)
+#undef FQ_PF_B
+        v4i a[4][2], xd[4];
+#define FQ_PF_A(mi)                                             \
+        a[mi][0] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab0);   \
+        a[mi][1] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab1);   \
+        xd[mi] = ds_read_b128_at<(mi) * 64>(xb);
+        FQ_PF_A(0) FQ_PF_A(1) FQ_PF_A(2) FQ_PF_A(3)
+#undef FQ_PF_A
+        asm volatile("s_waitcnt lgkmcnt(12)"
+                     : "+v"(pl[0][0]), "+v"(pl[0][1]), "+v"(pl[0][2]), "+v"(pl[1][0]), "+v"(pl[1][1]), "+v"(pl[1][2]),
+                       "+v"(pl[2][0]), "+v"(pl[2][1]), "+v"(pl[2][2]), "+v"(pl[3][0]), "+v"(pl[3][1]), "+v"(pl[3][2]),
+                       "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]));
         v4i b[4][2];
+        __half2 w2[4];
 #pragma unroll
         for (int ni = 0; ni < 4; ni++) {
-            const char *bsrc = buf + PF_A_BYTES + (wn * 4 + ni) * FQ_BLOCK + lane * 8;
-            const uint2 q0 = *reinterpret_cast<const uint2 *>(bsrc);
-            const uint2 q1 = *reinterpret_cast<const uint2 *>(bsrc + 512);
-            const uint2 q2 = *reinterpret_cast<const uint2 *>(bsrc + 1024);
-            b[ni][0] = unpack_fq6(q0.x, q1.x, q2.x);
-            b[ni][1] = unpack_fq6(q0.y, q1.y, q2.y);
+            b[ni][0] = unpack_fq6(pl[ni][0][0], pl[ni][1][0], pl[ni][2][0]);
+            b[ni][1] = unpack_fq6(pl[ni][0][1], pl[ni][1][1], pl[ni][2][1]);
+            w2[ni] = __half2half2(__ushort_as_half((uint16_t)wv[ni]));
         }
-        v4i acc[4][4];
 #pragma unroll
         for (int mi = 0; mi < 4; mi++) {
-            const int row = wm * 64 + mi * 16 + (lane & 15);
-            v4i a[2];
-#pragma unroll
-            for (int s = 0; s < 2; s++) a[s] = *reinterpret_cast<const v4i *>(buf + row * 128 + xswz(row, 4 * s + (lane >> 4)));
+            if (mi == 0) asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xd[0]));
+            if (mi == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xd[1]));
+            if (mi == 2) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[2][0]), "+v"(a[2][1]), "+v"(xd[2]));
+            if (mi == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[3][0]), "+v"(a[3][1]), "+v"(xd[3]));
+            const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)xd[mi][1], (uint32_t)xd[mi][0], 0x05040100u);
+            const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)xd[mi][3], (uint32_t)xd[mi][2], 0x05040100u);
 #pragma unroll
             for (int ni = 0; ni < 4; ni++) {
-                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[0], b[ni][0], v4i{0, 0, 0, 0}, 0, 0, 0);
-                acc[mi][ni] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[1], b[ni][1], acc[mi][ni], 0, 0, 0);
-            }
-        }
-
-        const uint16_t *sc = reinterpret_cast<const uint16_t *>(buf + PF_A_BYTES + PF_B_BYTES);
-#pragma unroll
-        for (int ni = 0; ni < 4; ni++) {
-            const int col = wn * 64 + ni * 16 + (lane & 15);
-            const __half2 w2 = __half2half2(__ushort_as_half(sc[PF_BM + col]));
-#pragma unroll
-            for (int mi = 0; mi < 4; mi++) {
-                const uint2 xv = *reinterpret_cast<const uint2 *>(sc + wm * 64 + mi * 16 + 4 * (lane >> 4));
-                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&xv.x), w2);
-                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&xv.y), w2);
+                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi][0], b[ni][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi][1], b[ni][1], acc, 0, 0, 0);
+                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&x01), w2[ni]);  // fp16-rounded
+                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&x23), w2[ni]);  // scale product
                 float *o = out[mi][ni];
-                const v4i &c = acc[mi][ni];
-                o[0] = fmaf((float)c[0], __low2float(p01), o[0]);
-                o[1] = fmaf((float)c[1], __high2float(p01), o[1]);
-                o[2] = fmaf((float)c[2], __low2float(p23), o[2]);
-                o[3] = fmaf((float)c[3], __high2float(p23), o[3]);
+                o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
+                o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
+                o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
+                o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
                 if (DBG) {
-                    const int n = t0 * 16 + col;
+                    const int n = (t0 + wn * 4 + ni) * 16 + (lane & 15);
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
                         const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + r;
-                        if (m < M && n < N) acc_dbg[((long)m * N + n) * G + g] = c[r] >> 2;
+                        if (m < M && n < N) acc_dbg[((size_t)m * N + n) * G + g] = acc[r] >> 2;
                     }
                 }
             }
         }
-        if (g + 1 < G) {
-            prefill_swrite(st, smem + ((g + 1) & 1) * PF_STAGE, tid);
-        }
-        __syncthreads();
+    };
+    stage(0, sb0);
+    stage(1, sb1);  // (G = 1: a never-read copy, like the refills past the last group below)
+    for (int g = 0; g < G; g += PF_DEPTH) {
+        kstep(g, sb0, sb2);
+        if (g + 1 < G) kstep(g + 1, sb1, sb0);
+        if (g + 2 < G) kstep(g + 2, sb2, sb1);
     }
+    // the refills past the last group are still landing: LDS must be quiet before the WG retires
+    __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
 
 #pragma unroll
     for (int mi = 0; mi < 4; mi++)
 #pragma unroll
         for (int ni = 0; ni < 4; ni++) {
-            const int n = t0 * 16 + wn * 64 + ni * 16 + (lane & 15);
+            const int n = (t0 + wn * 4 + ni) * 16 + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + r;
-                if (m < M && n < N) d[(long)m * N + n] = f2h(out[mi][ni][r] * 0.25f);
+                if (m < M && n < N) d[(size_t)m * N + n] = f2h(out[mi][ni][r] * 0.25f);
             }
         }
 }
@@ -876,13 +940,13 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         return acc_dbg ? dispatch_decode<false, true>(p, a, s) : dispatch_decode<false, false>(p, a, s);
     }
     const int NT = (N + 15) / 16;
-    dim3 grid((M + PF_BM - 1) / PF_BM, (NT + PF_BN / 16 - 1) / (PF_BN / 16));
-    const size_t lds = 2 * (size_t)PF_STAGE;
+    const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
+    if (nwg > 0x7fffffffL) return FQ_ERR_SHAPE;
     if (acc_dbg)
-        hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, grid, dim3(256), lds, s, xq, xs,
+        hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, dim3((unsigned)nwg), dim3(512), 0, s, xq, xs,
                            (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
     else
-        hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, grid, dim3(256), lds, s, xq, xs,
+        hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, dim3((unsigned)nwg), dim3(512), 0, s, xq, xs,
                            (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
     FQ_LAUNCH_CHECK();
     return FQ_OK;

@@ -330,3 +330,33 @@ def test_bmma_state_api_reference_layout(ops, dev):
     assert L.fq_bmma_exec(ctypes.byref(st), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
     ref, _, mag = oracle.gemm(xq, xs, wq, ws)
     assert_gemm_close(host(D), ref, mag, "bmma state api")
+
+
+@pytest.mark.parametrize("M,N,K,abits,with_acc", [
+    (1000, 1000, 1280, 6, True),      # ragged M and N (partial WG tiles on both edges)
+    (2048, 2048, 4096, 8, True),
+    (16384, 4096, 4096, 8, False),    # LLaMA-3-8B prefill (BASELINE C5) o_proj shape
+])
+def test_gemm_prefill_sampled(ops, dev, M, N, K, abits, with_acc):
+    """Prefill sizes: the whole GEMM on the GPU, the oracle on a seeded sample of rows x columns."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    lo, hi = -(1 << (abits - 1)), 1 << (abits - 1)
+    xq_d = torch.randint(lo, hi, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq_d = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs_d = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws_d = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq_d, ws_d)
+    out = ops.gemm_w6ax(xq_d, xs_d, pk, N, abits, return_acc=with_acc)
+    d, acc = out if with_acc else (out, None)
+    r = rng(M + K)
+    rows = np.sort(np.concatenate([r.choice(M, size=62, replace=False), [0, M - 1]]))
+    cols = np.sort(np.concatenate([r.choice(N, size=94, replace=False), [0, N - 1]]))
+    rows_t, cols_t = torch.from_numpy(rows).to(dev), torch.from_numpy(cols).to(dev)
+    xq, xs = host(xq_d.index_select(0, rows_t)), host(xs_d.index_select(1, rows_t))
+    wq, ws = host(wq_d.index_select(0, cols_t)), host(ws_d.index_select(1, cols_t))
+    ref, acc_ref, mag = oracle.gemm(np.ascontiguousarray(xq), np.ascontiguousarray(xs), wq,
+                                    np.ascontiguousarray(ws), want_acc=True)
+    if with_acc:
+        np.testing.assert_array_equal(host(acc.index_select(0, rows_t).index_select(1, cols_t)), acc_ref)
+    assert_gemm_close(host(d.index_select(0, rows_t).index_select(1, cols_t)), ref, mag,
+                      f"prefill M={M} N={N} K={K}")
