@@ -502,37 +502,57 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
 }
 
 // =============================================================================================
-// Prefill kernel (M > 32): int8-MFMA bound.  WG tile 256 (M) x 128 (N), 8 waves as 4 (M) x 2 (N),
-// each wave 64 x 64 = 4 x 4 tiles of 16x16; one k-step per 128-wide group.  Per group a stage holds
-//   A  256 rows x 128 B int8, 16-byte chunks XOR-swizzled by (row & 7) (xswz), so each 8-lane
-//      phase of a ds_read_b128 hits 8 distinct bank groups;
-//   B  the 8 fq6 blocks of the WG's 16-column tiles, verbatim (3 planes x 64 lanes x 8 B), read
-//      back as three ds_read_b64 per tile;
-//   the 256 x-scales (one per dword) and 128 w-scales of the group.
-// Staging is LDS-DMA only (global_load_lds: no VGPR round trip, no ds_write pass); three stages,
-// two in flight across the one raw barrier per group (counted vmcnt, never vmcnt(0) in the loop:
-// cdna_hip_programming.md "Pipelining across barriers").  Each wave issues PF_DMA DMA
-// instructions per stage: 4 of A (32 rows), 2 of B (waves 0-5) or of x-scales (waves 6-7), and
-// the w-scales (wave 7) or a filler.  Group accumulators are int32; dequant is one fp16 scale product and
-// one fp32 FMA per element and group, in the reference's order.
+// Prefill kernel (M > 32): int8-MFMA bound.  WG tile 128 (M) x 128 (N), 4 waves as 2 x 2, each
+// wave 64 x 64 = 4 x 4 tiles of 16x16; one k-step per 128-wide group; two WGs per CU, so that one
+// WG's barrier / LDS-latency chain overlaps the other's MFMAs.
+//
+// What bounds it (rocprofv3 + tools/prefill_ablate.py): the VALU beside the MFMAs and the serial
+// latency chain of each group step, not LDS or HBM bandwidth.  So:
+//   * the fq6 weights are unpacked ONCE per WG and group: each wave DMAs the three planes of two
+//     tiles (16 B per lane and plane = two block lanes, two groups ahead) into its own small LDS
+//     buffer, unpacks both k-steps at the start of the step before and writes the int8 B operands
+//     to LDS; every wave then reads ready MFMA operands;
+//   * A (128 rows x 128 B, 16-byte chunks XOR-swizzled by row & 7, xswz) and the group's scales
+//     arrive by LDS-DMA (global_load_lds, 16 B per lane), one group ahead, two stages;
+//   * the MFMA takes the weights as its A operand and the activations as B, so each lane ends with
+//     4 consecutive output columns of one row: 8-byte output stores, and the w-scales of those
+//     columns are one 8-byte LDS read;
+//   * dequant per element and group: one v_cvt_f32_i32 and one v_fma_mix_f32 with the fp16 scale
+//     product (half(xs * ws), two per v_pk_mul_f16) -- the reference's rounding.
+// One raw barrier per group.  Every wave issues 8 DMA instructions per group (4 of A, one of
+// scales or a filler, 3 weight planes).  All LDS accesses are inline asm: the compiler cannot
+// tell them from the DMA still landing and would drain it with vmcnt(0); waits are counted here.
 // =============================================================================================
-constexpr int PF_BM = 256, PF_BN = 128, PF_TILES = PF_BN / 16;
-constexpr int PF_A_BYTES = PF_BM * FQ_GROUP;              // 32 KiB
-constexpr int PF_B_OFF = PF_A_BYTES;
-constexpr int PF_XS_OFF = PF_B_OFF + PF_TILES * FQ_BLOCK;  // + 12 KiB
-constexpr int PF_WS_OFF = PF_XS_OFF + PF_BM * 4;           // x-scales one per dword
-constexpr int PF_PAD_OFF = PF_WS_OFF + PF_BN * 2;          // filler DMA target (never read)
-constexpr int PF_STAGE = PF_PAD_OFF + 16;                  // 46352 B
-constexpr int PF_DEPTH = 3;                                // 139056 B of LDS: one WG per CU
-constexpr int PF_DMA = 7;                                  // DMA instructions per wave and stage
+constexpr int PF_BM = 128, PF_BN = 128, PF_TILES = PF_BN / 16, PF_WAVES = 4;
+constexpr int PF_XS_OFF = PF_BM * FQ_GROUP;        // A: 16 KiB, then the x-scales, one per dword
+constexpr int PF_WS_OFF = PF_XS_OFF + PF_BM * 4;   // w-scales of the 8 tiles (fp16 [8][16])
+constexpr int PF_PAD_OFF = PF_WS_OFF + PF_BN * 2;  // filler DMA target (never read)
+constexpr int PF_ASTAGE = PF_PAD_OFF + 16;         // 17168 B, two stages
+constexpr int PF_BSTAGE = PF_TILES * 2 * 1024;     // unpacked B: [tile][k-step][lane][16 B], two stages
+constexpr int PF_VM_A = 5, PF_VM_W = 3;            // per wave and group: A + scale DMAs, weight planes
 // s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
 constexpr int vmcnt_only(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
-template <bool DBG>
-__global__ __launch_bounds__(512, 1) void fq_gemm_prefill_kernel(
+__device__ __forceinline__ void ds_write_b128(uint32_t a, v4i v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t ds_read_b32_at(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+}
+
+// ABL (development ablations, FQ_DEV_ABLATION builds only): 1 = no dequant (accumulators kept
+// alive, no VALU), 2 = no MFMA (operands kept alive), 4 = no compute-side LDS reads, 8 = no
+// global loads / DMA, 16 = no output stores, 32 = no A DMA, 64 = no weight loads.
+template <bool DBG, int ABL = 0>
+__global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
     int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg) {
-    __shared__ __attribute__((aligned(16))) char sb0[PF_STAGE], sb1[PF_STAGE], sb2[PF_STAGE];
+    __shared__ __attribute__((aligned(16))) char sa[2 * PF_ASTAGE];
+    __shared__ __attribute__((aligned(16))) char sbu[2 * PF_BSTAGE];
+    __shared__ __attribute__((aligned(16))) char sraw[PF_WAVES * 3072];
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
     const int lane = threadIdx.x & 63;
@@ -549,7 +569,7 @@ __global__ __launch_bounds__(512, 1) void fq_gemm_prefill_kernel(
     const int bm = first + (lid % span) % gsz, bn = (lid % span) / gsz;
     const int m0 = bm * PF_BM, t0 = bn * PF_TILES;
 
-    // ---- per-lane DMA sources at group 0 (a group adds 128 B to A, 1536 B to B, M or 16 to scales)
+    // ---- per-lane sources at group 0 (a group adds 128 B to A, 1536 B to B, M or 16 to scales)
     const int8_t *asrc[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -557,52 +577,69 @@ __global__ __launch_bounds__(512, 1) void fq_gemm_prefill_kernel(
         const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M are computed, never stored
         asrc[i] = xq + (size_t)m * K + ((lane & 7) ^ (row & 7)) * 16;
     }
-    const char *bsrc[2] = {nullptr, nullptr};
-    const uint16_t *ssrc[2] = {nullptr, nullptr};
-    if (wid < 6) {
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int o = (2 * wid + i) * 1024 + lane * 16;  // byte of the stage's B image
-            const int nt = o / FQ_BLOCK, t = t0 + nt < NT ? t0 + nt : NT - 1;
-            bsrc[i] = reinterpret_cast<const char *>(wpk) + (size_t)t * G * FQ_BLOCK + (o - nt * FQ_BLOCK);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int row = 128 * (wid - 6) + 64 * i + lane;
-            ssrc[i] = xs + (m0 + row < M ? m0 + row : M - 1);
-        }
-    }
-    const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;
+    const int srow = 64 * (wid & 1) + lane;  // waves 0-1: x-scales of rows 64w .. 64w + 63
+    const uint16_t *xsrc = xs + (m0 + srow < M ? m0 + srow : M - 1);
+    const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;  // wave 2: the w-scales
     const uint16_t *wsrc = wsb + (size_t)wt * G * 16 + 8 * (lane & 1);
+    const int btile = 2 * wid + (lane >> 5);  // tiles 2w, 2w + 1; block lanes 2j, 2j + 1
+    const int bt = t0 + btile < NT ? t0 + btile : NT - 1;
+    const char *bsrc = reinterpret_cast<const char *>(wpk) + (size_t)bt * G * FQ_BLOCK + (lane & 31) * 16;
 
-    // LDS read offsets of the wave's A rows (xswz: row & 7 == lane & 7 for every 16-row tile) and
-    // of its 4 x-scales per tile
-    const int arow = wm * 64 + (lane & 15);
-    const uint32_t a_off[2] = {(uint32_t)(arow * FQ_GROUP + xswz(arow, lane >> 4)),
-                               (uint32_t)(arow * FQ_GROUP + xswz(arow, 4 + (lane >> 4)))};
-    const uint32_t x_off = PF_XS_OFF + (wm * 64 + 4 * (lane >> 4)) * 4;
-
-    auto stage = [&](int g, char *buf) {
+    const uint32_t la = lds_addr(sa), lbu = lds_addr(sbu);
+    auto stage = [&](int g, int slot) {  // A + scales of group g -> A stage `slot` (PF_VM_A)
+        if (ABL & 8) return;
+        char *buf = sa + slot * PF_ASTAGE;
 #pragma unroll
         for (int i = 0; i < 4; i++)
-            __builtin_amdgcn_global_load_lds(asrc[i] + g * FQ_GROUP, LDS_PTR(buf + (32 * wid + 8 * i) * FQ_GROUP), 16, 0, 0);
-        if (wid < 6) {
+            if (!(ABL & 32))
+                __builtin_amdgcn_global_load_lds(asrc[i] + g * FQ_GROUP, LDS_PTR(buf + (32 * wid + 8 * i) * FQ_GROUP), 16, 0, 0);
+        if (wid < 2)
+            __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PF_XS_OFF + 64 * wid * 4), 2, 0, 0);
+        else if (lane < (wid == 2 ? 16 : 1))
+            __builtin_amdgcn_global_load_lds(wsrc + (wid == 2 ? g * 16 : 0), LDS_PTR(buf + (wid == 2 ? PF_WS_OFF : PF_PAD_OFF)), 16, 0, 0);
+    };
+    // The weight planes go through a small per-wave LDS buffer (DMA like A): values loaded into
+    // VGPRs by inline asm a whole step before their use would be invisible to the register
+    // allocator's notion of time, so a copy or re-use of those registers could race the load.
+    // Wave w's buffer is [plane][tile 2w, 2w + 1][512 B] (the DMA is lane-linear, 16 B = block
+    // lanes 2j, 2j + 1 per lane); each lane then reads back the 8-byte pieces of ITS block lane in
+    // both tiles, so that the unpacked operands are written lane-linearly (no bank conflicts).
+    const uint32_t lraw = lds_addr(sraw) + wid * 3072 + lane * 8;
+    auto load_w = [&](int g) {  // three planes of group g -> the wave's raw buffer (PF_VM_W)
+        if (ABL & (8 | 64)) return;
 #pragma unroll
-            for (int i = 0; i < 2; i++)
-                __builtin_amdgcn_global_load_lds(bsrc[i] + (size_t)g * FQ_BLOCK, LDS_PTR(buf + PF_B_OFF + (2 * wid + i) * 1024), 16, 0, 0);
-        } else {
+        for (int r = 0; r < 3; r++)
+            __builtin_amdgcn_global_load_lds(bsrc + (size_t)g * FQ_BLOCK + r * 512, LDS_PTR(sraw + wid * 3072 + r * 1024), 16, 0, 0);
+    };
+    v2u raw[2][3];  // [tile 2w + t][plane]
+    auto read_w = [&]() {  // the wave's raw buffer (landed) -> registers
+        raw[0][0] = ds_read_b64_at<0>(lraw);
+        raw[0][1] = ds_read_b64_at<1024>(lraw);
+        raw[0][2] = ds_read_b64_at<2048>(lraw);
+        raw[1][0] = ds_read_b64_at<512>(lraw);
+        raw[1][1] = ds_read_b64_at<1536>(lraw);
+        raw[1][2] = ds_read_b64_at<2560>(lraw);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(raw[0][0]), "+v"(raw[0][1]), "+v"(raw[0][2]), "+v"(raw[1][0]), "+v"(raw[1][1]), "+v"(raw[1][2])::"memory");
+    };
+    auto unpack_w = [&](int bslot) {  // raw -> int8 B operands of tiles 2w, 2w + 1, both k-steps
+        const uint32_t wa = lbu + bslot * PF_BSTAGE + 2 * wid * 2048 + lane * 16;
 #pragma unroll
-            for (int i = 0; i < 2; i++)
-                __builtin_amdgcn_global_load_lds(ssrc[i] + (size_t)g * M, LDS_PTR(buf + PF_XS_OFF + (128 * (wid - 6) + 64 * i) * 4), 2, 0, 0);
+        for (int t = 0; t < 2; t++) {
+            ds_write_b128(wa + t * 2048, unpack_fq6(raw[t][0][0], raw[t][1][0], raw[t][2][0]));
+            ds_write_b128(wa + t * 2048 + 1024, unpack_fq6(raw[t][0][1], raw[t][1][1], raw[t][2][1]));
         }
-        // the w-scales (wave 7, 16 lanes), or one 4-byte filler DMA into the pad word, so that every
-        // wave issues the same PF_DMA instructions per stage and one counted wait serves all paths
-        if (lane < (wid == 7 ? 16 : 1))
-            __builtin_amdgcn_global_load_lds(wsrc + (wid == 7 ? g * 16 : 0), LDS_PTR(buf + (wid == 7 ? PF_WS_OFF : PF_PAD_OFF)), 16, 0, 0);
     };
 
-    float out[4][4][4];
+    // LDS read offsets: the wave's A rows (xswz: row & 7 == lane & 7 for every 16-row tile), the
+    // x-scale of the lane's row per tile, its B operands and the w-scales of its 4 columns per tile
+    const int arow = wm * 64 + (lane & 15);
+    const uint32_t a_off0 = arow * FQ_GROUP + xswz(arow, lane >> 4), a_off1 = arow * FQ_GROUP + xswz(arow, 4 + (lane >> 4));
+    const uint32_t x_off = PF_XS_OFF + arow * 4;
+    const uint32_t w_off = PF_WS_OFF + (wn * 64 + 4 * (lane >> 4)) * 2;
+    const uint32_t b_off = wn * 4 * 2048 + lane * 16;
+
+    float out[4][4][4];  // [mi][ni][r]: row 16 mi + (lane & 15), column 16 ni + 4 (lane >> 4) + r
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
@@ -610,110 +647,129 @@ __global__ __launch_bounds__(512, 1) void fq_gemm_prefill_kernel(
 #pragma unroll
             for (int r = 0; r < 4; r++) out[i][j][r] = 0.f;
 
-    // One k-step: wait for stage g, barrier, refill the buffer stage g - 1 used with stage g + 2,
-    // compute on stage g.  The loop is unrolled by the stage count so that every buffer is a
-    // distinct __shared__ object: the compiler's wait insertion then sees that the ds_reads of
-    // stage g cannot alias the DMA still landing in the other two buffers (with one array it
-    // emits vmcnt(0) before the first ds_read of every k-step and drains the pipeline).
-    auto kstep = [&](int g, const char *buf, char *refill) {
-        // stage g landed for every wave (own count, then the barrier), and every wave is done
-        // reading stage g - 1, whose buffer the DMA below refills
-        // (the builtin, not inline asm: the compiler's own wait insertion accounts for it)
-        // Every step issues one stage (past the last group: a copy of it into a buffer no step reads
-        // again), so the same count holds on every path: stage g + 1 may stay in flight.
-        __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_DMA));
+    // prologue: A stage 0 and the weights of group 0; unpack them; weights of group 1
+    stage(0, 0);
+    load_w(0);
+    __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
+    read_w();
+    load_w(G > 1 ? 1 : 0);
+    unpack_w(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // Step g: barrier (A stage g, B operands g in LDS; every wave done with step g - 1) -> issue A
+    // stage g + 1 -> the weights of group g + 1 (loaded a step ago) to registers, their buffer
+    // refilled with group g + 2, unpacked to LDS -> MFMAs on group g -> wait for A stage g + 1.
+    for (int g = 0; g < G; g++) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        stage(g + 2 < G ? g + 2 : G - 1, refill);
+        stage(g + 1 < G ? g + 1 : G - 1, (g + 1) & 1);  // past the last group: never-read copies,
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_VM_A));  // so every path issues the same count
+        read_w();
+        load_w(g + 2 < G ? g + 2 : G - 1);
+        unpack_w((g + 1) & 1);
 
-        // LDS reads are inline asm (the compiler's wait insertion cannot tell them from the DMA
-        // landing in the other buffers and would drain it with vmcnt(0)); their lgkmcnt waits are
-        // counted here and re-define the loaded registers, so no use can move above its wait.
-        // Issue order: B planes + w-scales (16), then A + x-scales per 16-row tile (4 x 3).
-        const uint32_t lb = lds_addr(buf);
-        const uint32_t bb = lb + wn * 4 * FQ_BLOCK + lane * 8;
-        const uint32_t wb = lb + (wn * 64 + (lane & 15)) * 2;
-        const uint32_t ab0 = lb + a_off[0], ab1 = lb + a_off[1], xb = lb + x_off;
-        v2u pl[4][3];
-        uint32_t wv[4];
-#define FQ_PF_B(ni)                                                      \
-        pl[ni][0] = ds_read_b64_at<PF_B_OFF + (ni) * FQ_BLOCK>(bb);       \
-        pl[ni][1] = ds_read_b64_at<PF_B_OFF + (ni) * FQ_BLOCK + 512>(bb); \
-        pl[ni][2] = ds_read_b64_at<PF_B_OFF + (ni) * FQ_BLOCK + 1024>(bb); \
-        wv[ni] = ds_read_u16_at<PF_WS_OFF + (ni) * 32>(wb);
+        const uint32_t ab = la + (g & 1) * PF_ASTAGE, bb = lbu + (g & 1) * PF_BSTAGE + b_off;
+        v4i b[4][2];
+        v2u wv[4];
+        v4i a[4][2];
+        uint32_t xv[4];
+        if (ABL & 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                b[i][0] = b[i][1] = a[i][0] = a[i][1] = v4i{(int)ab, (int)bb, g, i};
+                wv[i] = v2u{ab + i, bb};
+                xv[i] = bb + i;
+            }
+        } else {
+#define FQ_PF_B(ni)                                                \
+        b[ni][0] = ds_read_b128_at<(ni) * 2048>(bb);                \
+        b[ni][1] = ds_read_b128_at<(ni) * 2048 + 1024>(bb);         \
+        wv[ni] = ds_read_b64_at<(ni) * 32>(ab + w_off);
         FQ_PF_B(0) FQ_PF_B(1) FQ_PF_B(2) FQ_PF_B(3)
 #undef FQ_PF_B
-        v4i a[4][2], xd[4];
-#define FQ_PF_A(mi)                                             \
-        a[mi][0] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab0);   \
-        a[mi][1] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab1);   \
-        xd[mi] = ds_read_b128_at<(mi) * 64>(xb);
+#define FQ_PF_A(mi)                                                    \
+        a[mi][0] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off0); \
+        a[mi][1] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off1); \
+        xv[mi] = ds_read_b32_at<(mi) * 64>(ab + x_off);
         FQ_PF_A(0) FQ_PF_A(1) FQ_PF_A(2) FQ_PF_A(3)
 #undef FQ_PF_A
-        asm volatile("s_waitcnt lgkmcnt(12)"
-                     : "+v"(pl[0][0]), "+v"(pl[0][1]), "+v"(pl[0][2]), "+v"(pl[1][0]), "+v"(pl[1][1]), "+v"(pl[1][2]),
-                       "+v"(pl[2][0]), "+v"(pl[2][1]), "+v"(pl[2][2]), "+v"(pl[3][0]), "+v"(pl[3][1]), "+v"(pl[3][2]),
-                       "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]));
-        v4i b[4][2];
-        __half2 w2[4];
-#pragma unroll
-        for (int ni = 0; ni < 4; ni++) {
-            b[ni][0] = unpack_fq6(pl[ni][0][0], pl[ni][1][0], pl[ni][2][0]);
-            b[ni][1] = unpack_fq6(pl[ni][0][1], pl[ni][1][1], pl[ni][2][1]);
-            w2[ni] = __half2half2(__ushort_as_half((uint16_t)wv[ni]));
         }
+        // (the 4 unpack writes are older than these reads: the counts below cover them)
+        asm volatile("s_waitcnt lgkmcnt(12)"
+                     : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]),
+                       "+v"(b[3][0]), "+v"(b[3][1]), "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]));
 #pragma unroll
         for (int mi = 0; mi < 4; mi++) {
-            if (mi == 0) asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xd[0]));
-            if (mi == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xd[1]));
-            if (mi == 2) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[2][0]), "+v"(a[2][1]), "+v"(xd[2]));
-            if (mi == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[3][0]), "+v"(a[3][1]), "+v"(xd[3]));
-            const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)xd[mi][1], (uint32_t)xd[mi][0], 0x05040100u);
-            const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)xd[mi][3], (uint32_t)xd[mi][2], 0x05040100u);
+            if (mi == 0) asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
+            if (mi == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xv[1]));
+            if (mi == 2) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[2][0]), "+v"(a[2][1]), "+v"(xv[2]));
+            if (mi == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[3][0]), "+v"(a[3][1]), "+v"(xv[3]));
+            const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);  // half2(xs, xs)
+            const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
 #pragma unroll
             for (int ni = 0; ni < 4; ni++) {
-                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi][0], b[ni][0], v4i{0, 0, 0, 0}, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mi][1], b[ni][1], acc, 0, 0, 0);
-                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&x01), w2[ni]);  // fp16-rounded
-                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&x23), w2[ni]);  // scale product
+                if (ABL & 2) {
+                    asm volatile("" ::"v"(a[mi][0]), "v"(a[mi][1]), "v"(b[ni][0]), "v"(b[ni][1]), "v"(x2u), "v"(wv[ni]));
+                    continue;
+                }
+                // weights as the A operand: acc[r] = column 4 (lane >> 4) + r, row lane & 15
+                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
+                if (ABL & 1) {
+                    asm volatile("" ::"v"(acc), "v"(x2u), "v"(wv[ni]));
+                    continue;
+                }
+                const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);  // fp16-rounded
+                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);  // scale product
                 float *o = out[mi][ni];
                 o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
                 o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
                 o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
                 o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
                 if (DBG) {
-                    const int n = (t0 + wn * 4 + ni) * 16 + (lane & 15);
+                    const int m = m0 + arow + mi * 16;
+                    const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
 #pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + r;
-                        if (m < M && n < N) acc_dbg[((size_t)m * N + n) * G + g] = acc[r] >> 2;
-                    }
+                    for (int r = 0; r < 4; r++)
+                        if (m < M && n + r < N) acc_dbg[((size_t)m * N + n + r) * G + g] = acc[r] >> 2;
                 }
             }
         }
-    };
-    stage(0, sb0);
-    stage(1, sb1);  // (G = 1: a never-read copy, like the refills past the last group below)
-    for (int g = 0; g < G; g += PF_DEPTH) {
-        kstep(g, sb0, sb2);
-        if (g + 1 < G) kstep(g + 1, sb1, sb0);
-        if (g + 2 < G) kstep(g + 2, sb2, sb1);
+        // A stage g + 1 landed (the weights of group g + 2 may stay in flight); the unpack writes
+        // retired with the reads above.  (sched_barrier: keep the wait below the MFMA block.)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_VM_W));
     }
-    // the refills past the last group are still landing: LDS must be quiet before the WG retires
+    // the copies past the last group are still landing: LDS must be quiet before the WG retires
     __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
 
+    // 4 consecutive columns per lane: one 8-byte store when N keeps them 8-byte aligned
+    const bool vec = (N & 3) == 0;
 #pragma unroll
-    for (int mi = 0; mi < 4; mi++)
+    for (int mi = 0; mi < 4; mi++) {
+        const int m = m0 + arow + mi * 16;
 #pragma unroll
         for (int ni = 0; ni < 4; ni++) {
-            const int n = (t0 + wn * 4 + ni) * 16 + (lane & 15);
+            const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
+            const float *o = out[mi][ni];
+            if (ABL & 16) {
+                asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+            } else if (m < M) {
+                uint16_t *dst = d + (size_t)m * N + n;
+                if (vec && n + 3 < N) {
+                    const uint32_t lo = (uint32_t)f2h(o[0] * 0.25f) | ((uint32_t)f2h(o[1] * 0.25f) << 16);
+                    const uint32_t hi = (uint32_t)f2h(o[2] * 0.25f) | ((uint32_t)f2h(o[3] * 0.25f) << 16);
+                    *reinterpret_cast<uint2 *>(dst) = make_uint2(lo, hi);
+                } else {
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int m = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + r;
-                if (m < M && n < N) d[(size_t)m * N + n] = f2h(out[mi][ni][r] * 0.25f);
+                    for (int r = 0; r < 4; r++)
+                        if (n + r < N) dst[r] = f2h(o[r] * 0.25f);
+                }
             }
         }
+    }
 }
 
 // =============================================================================================
@@ -942,11 +998,25 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
     const int NT = (N + 15) / 16;
     const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
     if (nwg > 0x7fffffffL) return FQ_ERR_SHAPE;
+#ifdef FQ_DEV_ABLATION
+    if (!acc_dbg && dev_ablation() >= 1 && dev_ablation() <= 127) {
+        const int abl = dev_ablation();
+#define FQ_PABL(v)                                                                                         \
+        if (abl == v)                                                                                        \
+            hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, v>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs, \
+                               (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
+        FQ_PABL(1) FQ_PABL(2) FQ_PABL(3) FQ_PABL(4) FQ_PABL(5) FQ_PABL(7) FQ_PABL(8) FQ_PABL(11) FQ_PABL(15)
+        FQ_PABL(16) FQ_PABL(31) FQ_PABL(35) FQ_PABL(67) FQ_PABL(99)
+#undef FQ_PABL
+        FQ_LAUNCH_CHECK();
+        return FQ_OK;
+    }
+#endif
     if (acc_dbg)
-        hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, dim3((unsigned)nwg), dim3(512), 0, s, xq, xs,
+        hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs,
                            (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
     else
-        hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, dim3((unsigned)nwg), dim3(512), 0, s, xq, xs,
+        hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs,
                            (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
