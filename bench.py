@@ -246,13 +246,20 @@ def main():
     if world > 1:
         dist.barrier()
 
-    if a.no_graph:
+    graph = None
+    if not a.no_graph:
+        try:
+            graph = capture(lambda: run_step(stack, M, world), stream)
+        except RuntimeError as e:  # (an RCCL build that cannot be captured: time eager launches)
+            if world == 1:
+                raise
+            print(f"[bench] rank {rank}: graph capture with RCCL failed ({e}); eager launches", file=sys.stderr)
+            torch.cuda.synchronize()
+    if graph is None:
         def replay():
             with torch.cuda.stream(stream):
                 run_step(stack, M, world)
     else:
-        graph = capture(lambda: run_step(stack, M, world), stream)
-
         def replay():
             graph.replay()
 
@@ -316,7 +323,7 @@ def main():
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
             "parallelism": f"tp{world} column-parallel + RCCL all-gather per linear" if world > 1 else "single GPU",
-            "graph": not a.no_graph,
+            "graph": graph is not None,
             "launches_per_layer": [[name, N, K, ab] for (name, N, K, ab) in launch_lins],
         },
         "roofline": {

@@ -1,0 +1,34 @@
+# Regenerates the committed profiles/ for the current code (run on the GPU box via gpurun).
+# usage: bash tools/profile_round.sh rNN   (then: cp gpurun_out/profiles/rNN_* profiles/)
+set -e
+R=${1:-r01}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/prof gpurun_out/profiles
+P=gpurun_out/profiles  # merged back by gpurun; copy into profiles/ afterwards
+B="python3 bench.py --cpu-budget 0 --no-fp16-compare"
+# 1. kernel trace + stats of the default bench (LLaMA-2-7B, M=1)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/kt -o run -- $B --steps 5 > gpurun_out/prof/kt.log 2>&1
+cp gpurun_out/prof/kt/run_kernel_stats.csv $P/${R}_kernel_stats.csv
+python3 tools/trace_summary.py gpurun_out/prof/kt/run_kernel_trace.csv > $P/${R}_kernel_trace_summary.txt
+tail -1 gpurun_out/prof/kt.log > $P/${R}_bench_under_rocprof.json
+# 2. HBM traffic: FETCH_SIZE pass alone (no other counters), decode kernel only
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_decode -f csv -d gpurun_out/prof/pmc -o run -- $B --steps 2 --warmup 1 --roofline-reps 1 > gpurun_out/prof/pmc.log 2>&1
+cp gpurun_out/prof/pmc/run_counter_collection.csv $P/${R}_pmc_fetch_size.csv
+python3 tools/pmc_summary.py $P/${R}_pmc_fetch_size.csv fq_gemm_decode llama2-7b-m1 $P/${R}_pmc_summary.json > /dev/null
+python3 - "$R" <<'PY'
+import json, sys
+p = f"gpurun_out/profiles/{sys.argv[1]}_pmc_summary.json"
+d = json.load(open(p))
+d.update(launch_pattern="qkv, o, gate_up (merged), down per layer", merged_gate_up=True,
+         command="rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_decode -f csv -- "
+                 "python3 bench.py --cpu-budget 0 --no-fp16-compare --steps 2 --warmup 1 --roofline-reps 1")
+d["source"] = f"profiles/{sys.argv[1]}_pmc_fetch_size.csv"  # where it is committed
+json.dump(d, open(p, "w"), indent=1)
+PY
+# 3. batch-16 config and the prefill GEMM (kernel stats)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/m16 -o run -- $B --config llama2-7b-m16 --steps 5 > gpurun_out/prof/m16.log 2>&1
+python3 tools/trace_summary.py gpurun_out/prof/m16/run_kernel_trace.csv > $P/${R}_m16_kernel_trace_summary.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/pf -o run -- python3 tools/prefill_bench.py 16384 > gpurun_out/prof/pf.log 2>&1
+python3 tools/trace_summary.py gpurun_out/prof/pf/run_kernel_trace.csv > $P/${R}_prefill_kernel_trace_summary.txt
+cp gpurun_out/prof/pf.log $P/${R}_prefill_bench.txt
+echo profiles done
