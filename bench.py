@@ -177,6 +177,41 @@ def pmc_traffic(config, merge):
     return None, None
 
 
+def calibrate_peaks(dev, hbm_bytes=4 << 30, mfma_iters=20000):
+    """Measured on this box: HBM streaming-read GB/s of a 16 B/lane
+    non-temporal read over 4 GiB, and dense int8 MFMA TOPS of 4 independent
+    v_mfma_i32_16x16x64_i8 chains per wave, 2 waves per SIMD (tools/fq_calib.hip)."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libfq_calib.so"))
+    lib.fqc_hbm_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    lib.fqc_mfma_i8.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    buf = torch.ones(hbm_bytes // 4, dtype=torch.int32, device=dev)
+    sink = torch.zeros(8 * cus, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    h = ctypes.c_void_p(s.cuda_stream)
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(reps):
+            fn()
+        b.record(s)
+        b.synchronize()
+        return a.elapsed_time(b) / 1e3 / reps
+
+    t_hbm = timed(lambda: lib.fqc_hbm_read(ctypes.c_void_p(buf.data_ptr()), ctypes.c_size_t(hbm_bytes),
+                                           ctypes.c_void_p(sink.data_ptr()), 8 * cus, h), 5)
+    t_mfma = timed(lambda: lib.fqc_mfma_i8(mfma_iters, cus, ctypes.c_void_p(sink.data_ptr()), h), 3)
+    del buf
+    ops_mfma = cus * 8 * 4 * mfma_iters * (16 * 16 * 64 * 2)
+    return {"hbm_read_GBps": round(hbm_bytes / t_hbm / 1e9, 1), "int8_mfma_TOPS": round(ops_mfma / t_mfma / 1e12, 1),
+            "method": "tools/fq_calib.hip: 4 GiB 16 B/lane non-temporal streaming read; 4 independent "
+                      "16x16x64 i8 MFMA chains per wave, 8 waves per CU"}
+
+
 def cpu_baseline(budget_s=15.0):
     """The reference's CPU fake-quant QuantLinear forward (oracle restatement, torch CPU ops) on a
     bounded sample: LLaMA-2-7B linear shapes at M=1, fp16, weights re-fake-quantised every forward
@@ -220,6 +255,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline (0 = skip)")
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
+    ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -303,6 +339,10 @@ def main():
     achieved = bytes_launch / per_launch_s / 1e9
     del g2
     traffic, traffic_src = pmc_traffic(a.config, merge) if world == 1 else (None, None)
+    if world > 1:  # the same step without the all-gathers (max over ranks)
+        tg = torch.tensor([t_g / a.roofline_reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        gemm_only_ms = float(tg.item()) * 1e3
 
     res = {
         "metric": "W6A6 GEMM TFLOPS-equiv + tok/s on LLaMA-2-7B linear shapes, 1/2/4/8 GPU",
@@ -342,17 +382,26 @@ def main():
             "method": "graph of the step's linear launches only (no all-gather), HIP events on the capture stream",
         },
     }
+    if world > 1:
+        res["gemm_only_ms_per_step"] = round(gemm_only_ms, 4)
+        res["allgather_bytes_per_step_per_rank"] = int(layers * sum(2 * M * (N // world) * (world - 1)
+                                                                    for (_, N, K, _) in launch_lins))
+    if world == 1 and not a.no_calibrate:
+        res["roofline"]["peak_measured"] = calibrate_peaks(dev)
+        res["roofline"]["frac_of_measured"] = round(achieved / res["roofline"]["peak_measured"]["hbm_read_GBps"], 4)
     if world == 1 and not a.no_fp16_compare:
         del stack
         torch.cuda.empty_cache()
         shapes = sorted({(N, K) for (_, N, K, _) in lins})
         cmp_cfg = fp16_compare(shapes, M, 6, dev)
-        cmp_ns = fp16_compare(NORTH_STAR_SHAPES, 1, 6, dev)
+        cmp_ns = {m: fp16_compare(NORTH_STAR_SHAPES, m, 6, dev) for m in (1, 2, 4, 8)}
         geo = lambda rows: round(float(np.exp(np.mean([np.log(r["speedup"]) for r in rows]))), 3)
         res["vs_rocblas_fp16"] = {
-            "what": "W6A6 linear (fused quantize+GEMM) vs torch F.linear fp16 (hipBLASLt/rocBLAS), same M,N,K, graph-timed",
+            "what": "W6A6 linear (quantize+GEMM, one launch where fused) vs torch F.linear fp16 "
+                    "(hipBLASLt/rocBLAS), same M,N,K, graph-timed",
             "config_shapes": cmp_cfg, "config_geomean_speedup": geo(cmp_cfg),
-            "llama2_70b_m1": cmp_ns, "llama2_70b_m1_geomean_speedup": geo(cmp_ns),
+            "llama2_70b_m1": cmp_ns[1], "llama2_70b_m1_geomean_speedup": geo(cmp_ns[1]),
+            "llama2_70b_geomean_speedup_by_M": {str(m): geo(r) for m, r in cmp_ns.items()},
             "north_star_target": 1.3,
         }
     if rank == 0 and world == 1 and a.cpu_budget > 0:
