@@ -59,6 +59,28 @@ __device__ __forceinline__ float max16(float m) {
     return m;
 }
 
+// The same 16-lane max for values that are -1.0 or non-negative (never NaN): their bit patterns
+// order like signed integers, so the reduction is four v_max_i32 with a DPP source (no NaN
+// canonicalisation around each step, which fmaxf needs).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float max16_nonneg(float m) {
+    int b = __float_as_int(m);
+    b = max(b, dpp_i32<0xB1>(b));
+    b = max(b, dpp_i32<0x4E>(b));
+    b = max(b, dpp_i32<0x141>(b));
+    b = max(b, dpp_i32<0x140>(b));
+    return __int_as_float(b);
+}
+
+__device__ __forceinline__ int med3_i32(int v, int lo, int hi) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(lo), "v"(hi));
+    return r;
+}
+
 // v_cvt_i32_f32: truncation with the hardware's saturation (out of range clamps, NaN -> 0),
 // the same results as CUDA's cvt.rzi.s32.f32 that the reference relies on.
 __device__ __forceinline__ int cvt_i32_sat(float v) {
@@ -73,13 +95,13 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
     const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
     const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
     v2f v[4];
-    float mx = -1.0f;
+    float mx = -1.0f;  // the reference's seed; fmaxf skips NaN inputs, so mx is never NaN
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         v[i] = v2f{h2f((uint16_t)wd[i]), h2f((uint16_t)(wd[i] >> 16))};
         mx = fmaxf(mx, fmaxf(fabsf(v[i].x), fabsf(v[i].y)));
     }
-    mx = max16(mx);
+    mx = max16_nonneg(mx);
     // IEEE fp32 absmax / hi as a Newton-corrected product with y = RN(1/hi): bit-identical over
     // every fp16 absmax (exhaustive: tests/test_oracle.py::test_quantizer_division_by_constant_is_exact)
     const float fhi = (float)hi, y = bits == 8 ? (float)(1.0 / 127.0) : (float)(1.0 / 31.0);
@@ -90,24 +112,40 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
     const float rc = __builtin_amdgcn_rcpf(r);
     const v2f r2 = {r, r}, rc2 = {rc, rc};
     // Newton step unless the scale is 0 / inf (then the plain product has the IEEE quotient's
-    // value class); wave-uniform in practice, so the common case carries no select.
+    // value class).  A wave-uniform branch: the common case carries no per-element select.
     const bool newton = __builtin_isfinite(r) && r != 0.0f;
     v2f q[4];
+    if (__builtin_amdgcn_ballot_w64(!newton) == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) {  // packed fp32 math: v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32
-        const v2f q1 = v[i] * rc2;
-        q[i] = q1;
-        if (newton) q[i] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, r2, v[i]), rc2, q1);
+        for (int i = 0; i < 4; i++) {  // packed fp32 math: v_pk_mul_f32 / v_pk_fma_f32
+            const v2f q1 = v[i] * rc2;
+            q[i] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, r2, v[i]), rc2, q1);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const v2f q1 = v[i] * rc2;
+            q[i] = q1;
+            if (newton) q[i] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, r2, v[i]), rc2, q1);
+        }
     }
-    uint32_t w[2] = {0, 0};
+    int c[8];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         // roundf = trunc(q + copysign(0.5, q)) here: q is either an exact half-integer or at
         // least 2^-12 (relative) away from one, so the addition cannot cross an integer; the
         // truncating, saturating v_cvt_i32_f32 then also maps +-inf to the int range, NaN to 0.
         const v2f t = q[i] + v2f{__builtin_copysignf(0.5f, q[i].x), __builtin_copysignf(0.5f, q[i].y)};
-        const int c0 = min(max(cvt_i32_sat(t.x), lo), hi), c1 = min(max(cvt_i32_sat(t.y), lo), hi);
-        w[i >> 1] |= ((uint32_t)(c0 & 255) | ((uint32_t)(c1 & 255) << 8)) << (16 * (i & 1));
+        c[2 * i] = med3_i32(cvt_i32_sat(t.x), lo, hi);
+        c[2 * i + 1] = med3_i32(cvt_i32_sat(t.y), lo, hi);
+    }
+    // low bytes of 8 codes -> 2 dwords (v_perm_b32: selector 0x0c = zero byte)
+    uint32_t w[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)c[4 * h + 1], (uint32_t)c[4 * h], 0x0c0c0400u);
+        const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)c[4 * h + 3], (uint32_t)c[4 * h + 2], 0x0c0c0400u);
+        w[h] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
     }
     codes = make_uint2(w[0], w[1]);
     return sh;

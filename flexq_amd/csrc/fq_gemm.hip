@@ -63,6 +63,20 @@ __device__ __forceinline__ uint32_t ds_read_u16_at(uint32_t a) {
     return v;
 }
 
+// s_waitcnt vmcnt(BASE + k) for a wave-uniform runtime k (immediates only); vmcnt(0) past 7
+template <int BASE>
+__device__ __forceinline__ void wait_vm_plus(int k) {
+#define FQ_WAIT_PLUS(j)                                                           \
+    if (k == (j) && BASE + (j) <= 63) {                                           \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(BASE + (j) <= 63 ? BASE + (j) : 0) : "memory"); \
+        return;                                                                   \
+    }
+    FQ_WAIT_PLUS(0) FQ_WAIT_PLUS(1) FQ_WAIT_PLUS(2) FQ_WAIT_PLUS(3) FQ_WAIT_PLUS(4) FQ_WAIT_PLUS(5)
+    FQ_WAIT_PLUS(6) FQ_WAIT_PLUS(7)
+#undef FQ_WAIT_PLUS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int U, int D>
 __device__ __forceinline__ void wait_ring(int later) {
     // s_waitcnt takes an immediate: `later` (< D) blocks of U DMA instructions may stay in flight
@@ -267,30 +281,36 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
         }
     };
 
-    if (n > 0 && !SS && !(ABL & 8)) {  // ---- prologue staging (issued first: the ring waits retire it in order)
-        for (int i0 = 0; i0 < n; i0 += 32) {  // w-scales: 32 blocks (32 B = 2 lanes each) per instruction
-            const int i = i0 + (lane >> 1) < n ? i0 + (lane >> 1) : n - 1;
-            __builtin_amdgcn_global_load_lds(wsb + ((long)item_tile(i / ng) * G + ga + i % ng) * 16 + 8 * (lane & 1),
-                                             LDS_PTR(ws_st + i0 * 32), 16, 0, 0);
-        }
-        if (!FUSE) {
-            for (int i0 = 0; i0 < ng; i0 += 64 / XSR) {  // x-scales: XSR per group, ushort per lane
-                const int i = i0 + lane / XSR, row = lane % XSR;
-                __builtin_amdgcn_global_load_lds(xs + (long)(ga + (i < ng ? i : ng - 1)) * M + (row < M ? row : M - 1),
-                                                 LDS_PTR(xs_st + i0 * XSR * 4), 2, 0, 0);
+    // ---- staging of the wave's scales (and unfused activation rows): issued right after the
+    // first ring block (below), so that every wave's first-needed DMAs leave the CU's address unit
+    // before the rest of the prologue burst; the first ring wait retires it in order.
+    const int nws = (n > 0 && !SS && !(ABL & 8)) ? (n + 31) / 32 : 0;  // its instruction count
+    auto stage_all = [&]() {
+        if (n > 0 && !SS && !(ABL & 8)) {
+            for (int i0 = 0; i0 < n; i0 += 32) {  // w-scales: 32 blocks (32 B = 2 lanes each) per instruction
+                const int i = i0 + (lane >> 1) < n ? i0 + (lane >> 1) : n - 1;
+                __builtin_amdgcn_global_load_lds(wsb + ((long)item_tile(i / ng) * G + ga + i % ng) * 16 + 8 * (lane & 1),
+                                                 LDS_PTR(ws_st + i0 * 32), 16, 0, 0);
+            }
+            if (!FUSE) {
+                for (int i0 = 0; i0 < ng; i0 += 64 / XSR) {  // x-scales: XSR per group, ushort per lane
+                    const int i = i0 + lane / XSR, row = lane % XSR;
+                    __builtin_amdgcn_global_load_lds(xs + (long)(ga + (i < ng ? i : ng - 1)) * M + (row < M ? row : M - 1),
+                                                     LDS_PTR(xs_st + i0 * XSR * 4), 2, 0, 0);
+                }
             }
         }
-    }
-    FQ_STAMP(7);
-    if (n > 0 && !XS && !FUSE && !(ABL & 8)) {  // activation rows: 8 lanes x 16 B per (group, row)
-        for (int r0 = 0; r0 < R; r0 += 8) {
-            const int rg = r0 + (lane >> 3) < R ? r0 + (lane >> 3) : R - 1;
-            const int j = rg / M, row = rg - j * M;
-            const int chunk = (lane & 7) ^ (row & 7);  // lands at position lane & 7 (xswz)
-            __builtin_amdgcn_global_load_lds(xq + (long)row * K + (long)(ga + j) * FQ_GROUP + chunk * 16,
-                                             LDS_PTR(x_st + r0 * 128), 16, 0, 0);
+        if (n > 0 && !XS && !FUSE && !(ABL & 8)) {  // activation rows: 8 lanes x 16 B per (group, row)
+            for (int r0 = 0; r0 < R; r0 += 8) {
+                const int rg = r0 + (lane >> 3) < R ? r0 + (lane >> 3) : R - 1;
+                const int j = rg / M, row = rg - j * M;
+                const int chunk = (lane & 7) ^ (row & 7);  // lands at position lane & 7 (xswz)
+                __builtin_amdgcn_global_load_lds(xq + (long)row * K + (long)(ga + j) * FQ_GROUP + chunk * 16,
+                                                 LDS_PTR(x_st + r0 * 128), 16, 0, 0);
+            }
         }
-    }
+        FQ_STAMP(7);
+    };
 
     // ---- the ring over the wave's block sequence
     const char *wbytes = reinterpret_cast<const char *>(wpk) + lane * 16;
@@ -313,10 +333,12 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
                 __builtin_amdgcn_global_load_lds(xs + (long)g * M + (lane < M ? lane : M - 1), LDS_PTR(dst + C::XS_OFF), 2, 0, 0);
         }
     };
-    // Order: staging (above) -> first activation window -> exactly D ring issues (unrolled; slots
-    // past a short sequence get a never-read copy of its last block).  Waiting for the window is
-    // then `vmcnt(D*U)`: everything younger is the ring.  (Each wave instruction costs the CU's
-    // address unit ~30 cycles whatever its size, so only instructions that carry data are issued.)
+    // Order: first activation window -> ring block 0 -> staging -> ring blocks 1 .. D-1 (exactly
+    // D ring issues, unrolled; slots past a short sequence get a never-read copy of its last
+    // block).  The first ring wait (vmcnt((D-1)U)) then retires block 0 and the staging, and
+    // waiting for the window is vmcnt(D*U + nws).  Each wave instruction costs the CU's address
+    // unit ~30 cycles whatever its size, and the prologue burst of all waves is ~60 of them: the
+    // first-needed ones go first.
     if (FUSE && n > 0) x_fetch(0);
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
     if (n > 0) {
@@ -327,12 +349,13 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
                 rj = 0;
                 ++rit;
             }
+            if (i == 0) stage_all();
         }
     }
     FQ_STAMP(1);
 
     if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(D * C::U) : "memory");
+        wait_vm_plus<D * C::U>(nws);
         FQ_STAMP(5);
         x_quant(0);
         FQ_STAMP(6);
