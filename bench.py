@@ -4,18 +4,20 @@ Workload (BASELINE.json configs[1]): LLaMA-2-7B, every linear layer of all 32 de
 W6A6 group 128, batch 1 (M = 1), random-init weights of that architecture, synthetic fp16
 activations resident in HBM.  One "step" = one token through the 32-layer linear stack: per
 layer 5 W6A6 linears (qkv 12288x4096, o 4096x4096, gate/up 11008x4096 reading the same input,
-down 4096x11008), each an fq_linear_w6ax call = dynamic activation quantization + GEMM + dequant
-(at decode sizes a single fused launch), captured into one HIP graph.  gate and up share their
+down 4096x11008), each = dynamic activation quantization + GEMM + dequant.  The linears form a
+dependency chain as in decoding (each reads the previous one's output).  gate and up share their
 input, so by default they run as one linear over the concatenated weight image [gate; up]
-(22016x4096, output [gate | up], per-column arithmetic unchanged): 4 launches per layer
-(--no-merge: 5).
+(22016x4096, output [gate | up], per-column arithmetic unchanged): 4 linears per layer
+(--no-merge: 5).  Default mode on one GPU (M <= 4): the whole step is ONE persistent launch
+(ops.LinearSeq / fq_linear_seq_run, fq_seq.hip) captured in a HIP graph; --mode launches: one
+fq_linear_w6ax launch per linear in a HIP graph (the JSON reports both on one GPU).
 
 Multi-GPU (torchrun, one process per GPU, RCCL): column-parallel N-shard of every linear, each
 rank packs and streams only its N/P rows, then ONE all-gather per linear of the dequantized
 fp16 output over xGMI.  Total work is fixed, so "scaling" is "strong".
 
-Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
-linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
+Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the chain
+launch, or the decode linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
 forward, timed on a bounded sample on this host).
 """
 import argparse
@@ -76,39 +78,56 @@ def launch_list(lins, merge):
 
 
 def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
+    """Random-init weights of the architecture and the step's data flow.  The linears form a real
+    dependency chain, as in decoding: the input of each linear is the leading M*K values of the
+    previous linear's output buffer (standing in for the out-of-scope attention / norm / SiLU
+    between them; gate and up read the same input), so every linear waits for the one before.
+    Weight scales give each linear unit gain, so values stay O(1) through all the layers."""
     layers, M, lins, _ = cfg
     g = torch.Generator(device=dev).manual_seed(seed + rank)
     stack = []
+    prev = torch.randn((M * lins[0][2],), dtype=torch.float16, device=dev, generator=g)  # the token
+    x_first = prev
     for _ in range(layers):
         L = {}
         for (name, N, K, abits) in launch_list(lins, merge):
             assert N % (16 * world) == 0, f"{name}: N={N} not divisible into 16-column shards for {world} ranks"
             Nl = N // world
             wq = torch.randint(-32, 32, (Nl, K), dtype=torch.int8, device=dev, generator=g)
-            ws = (torch.rand((K // GROUP, Nl), device=dev, generator=g) * 0.02 + 1e-3).half()
+            # codes have rms 18.5 and U(0.5, 1.5) has rms 1.04: unit gain per linear
+            ws = ((torch.rand((K // GROUP, Nl), device=dev, generator=g) + 0.5) / (18.5 * 1.04 * K ** 0.5)).half()
             pk = ops.pack_w6(wq, ws)  # the weight image: 6-bit codes + blocked group scales
             del wq, ws
             out = torch.empty((M, Nl), dtype=torch.float16, device=dev)
             full = torch.empty((world * M * Nl,), dtype=torch.float16, device=dev) if world > 1 else None
-            L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full)
-        # synthetic fp16 inputs of each linear (attention / activation outputs are out of scope)
-        for name in L:
-            if name != "up":  # up reads gate's input
-                L[name]["x"] = torch.randn((M, L[name]["K"]), dtype=torch.float16, device=dev, generator=g)
+            src = prev if name != "up" else L["gate"]["x"].view(-1)
+            x = src[:M * K].view(M, K)
+            L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full, x=x)
+            if name != "gate":
+                prev = (full if world > 1 else out).view(-1)
         stack.append(L)
+    stack[0]["_input"] = x_first
     return stack
 
 
+def linears(stack):
+    return [(n, p) for L in stack for n, p in L.items() if not n.startswith("_")]
+
+
 def run_step(stack, M, world, group=None, gather=True):
-    """One token through the linear stack: fq_linear_w6ax per linear (decode sizes: one fused
-    quantize+GEMM launch each; gate and up read the same input), then one RCCL all-gather of the
-    fp16 shard outputs per linear when world > 1."""
-    for L in stack:
-        for name, p in L.items():
-            x = L["gate" if name == "up" else name]["x"]
-            ops.linear_w6ax(x, p["pk"], p["Nl"], p["abits"], out=p["out"])
-            if world > 1 and gather:
-                dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
+    """One token through the linear stack, one launch per linear: fq_linear_w6ax (decode sizes:
+    one fused quantize+GEMM launch each), then one RCCL all-gather of the fp16 shard outputs per
+    linear when world > 1."""
+    for name, p in linears(stack):
+        ops.linear_w6ax(p["x"], p["pk"], p["Nl"], p["abits"], out=p["out"])
+        if world > 1 and gather:
+            dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
+
+
+def make_seq(stack):
+    """The whole step as ONE persistent launch (ops.LinearSeq, fq_linear_seq_*): the same
+    linears, the same data flow, dependencies derived from the buffers."""
+    return ops.LinearSeq([(p["x"], p["pk"], p["Nl"], p["abits"], p["out"]) for _, p in linears(stack)])
 
 
 def capture(fn, stream):
@@ -165,14 +184,14 @@ def fp16_compare(shapes, M, abits, dev, reps=20):
     return out
 
 
-def pmc_traffic(config, merge):
+def pmc_traffic(config, merge, mode):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 FETCH_SIZE
     pass for this workload (profiles/rNN_pmc_summary.json, written by tools/pmc_summary.py, with
     the gfx950 x2 correction applied).  None when no pass matches."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), reverse=True):
         d = json.load(open(path))
-        if d.get("config") == config and d.get("merged_gate_up", False) == merge:
+        if d.get("config") == config and d.get("merged_gate_up", False) == merge and d.get("mode", "launches") == mode:
             return d["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -256,6 +275,9 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
+    ap.add_argument("--mode", choices=["seq", "launches"], default=None,
+                    help="seq: the whole step as one persistent chain launch (default for one GPU, M <= 4); "
+                         "launches: one launch per linear (+ an RCCL all-gather each when world > 1)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,13 +293,22 @@ def main():
     layers, M, lins, desc = cfg
     merge = not a.no_merge
     launch_lins = launch_list(lins, merge)
+    mode = a.mode or ("seq" if world == 1 and M <= 4 else "launches")
+    assert mode == "launches" or (world == 1 and M <= 4), "--mode seq: one GPU, M <= 4"
     stack = build_stack(cfg, rank, world, dev, merge)
+    seq = make_seq(stack) if mode == "seq" else None
     stream = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
 
+    def step(gather=True):
+        if seq is not None:
+            seq.run()
+        else:
+            run_step(stack, M, world, gather=gather)
+
     # warm the per-stream workspace and RCCL communicators eagerly, on the capture stream
     with torch.cuda.stream(stream):
-        run_step(stack, M, world)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -285,7 +316,7 @@ def main():
     graph = None
     if not a.no_graph:
         try:
-            graph = capture(lambda: run_step(stack, M, world), stream)
+            graph = capture(step, stream)
         except RuntimeError as e:  # (an RCCL build that cannot be captured: time eager launches)
             if world == 1:
                 raise
@@ -294,7 +325,7 @@ def main():
     if graph is None:
         def replay():
             with torch.cuda.stream(stream):
-                run_step(stack, M, world)
+                step()
     else:
         def replay():
             graph.replay()
@@ -319,26 +350,40 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    last = linears(stack)[-1][1]["out"]
+    finite = bool(torch.isfinite(last.float()).all().item())
+    if seq is not None:
+        assert seq.error_word() == 0, "a dependency wait of the chain gave up"
 
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
     value = flops_step * a.steps / elapsed / 1e12
     tok_s = M * a.steps / elapsed
 
-    # roofline of the dominant kernel (the fused decode linear): a graph of the step's linear
-    # launches only (no all-gather), timed with HIP events on the capture stream
-    g2 = capture(lambda: run_step(stack, M, world, gather=False), stream)
-    for _ in range(2):
-        g2.replay()
-    torch.cuda.synchronize()
-    t_g = time_graph(g2, a.roofline_reps, stream)
-    launches = layers * len(launch_lins)
-    per_launch_s = t_g / (a.roofline_reps * launches)
-    fused = {(N, K): ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in launch_lins}
-    bytes_launch = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)])
-                                for (_, N, K, ab) in launch_lins) / launches
+    # roofline of the dominant kernel: a graph of the step's launches without the all-gathers
+    # (seq: the one chain launch; launches: the linears), timed with HIP events on its stream
+    fused = {(N, K): seq is not None or ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in launch_lins}
+    step_bytes = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins)
+
+    def graph_time(fn, launches):
+        g2 = capture(fn, stream)
+        for _ in range(2):
+            g2.replay()
+        torch.cuda.synchronize()
+        t = time_graph(g2, a.roofline_reps, stream)
+        del g2
+        return t, t / (a.roofline_reps * launches)
+
+    n_lin = layers * len(launch_lins)
+    t_g, per_launch_s = graph_time(lambda: step(gather=False), 1 if seq is not None else n_lin)
+    bytes_launch = step_bytes / (1 if seq is not None else n_lin)
     achieved = bytes_launch / per_launch_s / 1e9
-    del g2
-    traffic, traffic_src = pmc_traffic(a.config, merge) if world == 1 else (None, None)
+    per_linear = None
+    if seq is not None:  # the same step as one launch per linear, for comparison
+        _, pl = graph_time(lambda: run_step(stack, M, world, gather=False), n_lin)
+        per_linear = {"per_launch_us": round(pl * 1e6, 3), "ms_per_step": round(pl * n_lin * 1e3, 4),
+                      "achieved_GBps": round(step_bytes / n_lin / pl / 1e9, 1),
+                      "frac": round(step_bytes / n_lin / pl / 1e9 / HBM_PEAK_GBS, 4)}
+    traffic, traffic_src = pmc_traffic(a.config, merge, mode) if world == 1 else (None, None)
     if world > 1:  # the same step without the all-gathers (max over ranks)
         tg = torch.tensor([t_g / a.roofline_reps], dtype=torch.float64, device=dev)
         dist.all_reduce(tg, op=dist.ReduceOp.MAX)
@@ -356,10 +401,13 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int8-mfma(w6a6)->fp16",
-        "data": "synthetic (random-init int6 weights of the architecture, N(0,1) fp16 activations)",
+        "data": "synthetic (random-init int6 weights of the architecture with unit-gain scales; N(0,1) fp16 "
+                "token, each linear reading the previous linear's output)",
+        "outputs_finite": finite,
         "tok_per_s": round(tok_s, 2),
         "config": {
-            "workload": desc + ", linear stack of every decoder layer per step (HIP graph)",
+            "workload": desc + ", dependent linear stack of every decoder layer per step",
+            "mode": mode,
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
             "parallelism": f"tp{world} column-parallel + RCCL all-gather per linear" if world > 1 else "single GPU",
@@ -367,7 +415,9 @@ def main():
             "launches_per_layer": [[name, N, K, ab] for (name, N, K, ab) in launch_lins],
         },
         "roofline": {
-            "kernel": "fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else "fq_gemm_decode_kernel (+ quantize where unfused)",
+            "kernel": ("fq_seq_kernel (the whole step: one launch)" if seq is not None else
+                       "fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else
+                       "fq_gemm_decode_kernel (+ quantize where unfused)"),
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -379,9 +429,11 @@ def main():
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
             "fused_launches": all(fused.values()),
-            "method": "graph of the step's linear launches only (no all-gather), HIP events on the capture stream",
+            "method": "graph of the step's launches only (no all-gather), HIP events on the capture stream",
         },
     }
+    if per_linear is not None:
+        res["roofline"]["one_launch_per_linear"] = per_linear
     if world > 1:
         res["gemm_only_ms_per_step"] = round(gemm_only_ms, 4)
         res["allgather_bytes_per_step_per_rank"] = int(layers * sum(2 * M * (N // world) * (world - 1)

@@ -13,89 +13,7 @@
 // B[k = 16*(l>>4) + j][col l&15], j = 0..15 -- any k relabelling shared by A and B gives the same
 // sum; C/D: col = l&15, row = 4*(l>>4) + r, r = 0..3 (cdna_hip_programming.md §3).  The fq6
 // weight layout stores exactly these B operands (16-column tiles, fq_quant.hip).
-#include "fq_common.h"
-
-#define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)(p);
-}
-__device__ __forceinline__ v4i ds_read_b128(uint32_t a) {
-    v4i v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-typedef unsigned v2u __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ v2u ds_read_b64(uint32_t a) {
-    v2u v;
-    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-__device__ __forceinline__ void ds_write_b64(uint32_t a, uint2 v) {
-    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ void ds_write_b32(uint32_t a, uint32_t v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-__device__ __forceinline__ uint32_t ds_read_u16(uint32_t a) {
-    uint32_t v;
-    asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-
-// immediate-offset forms (offset < 64 KiB folded into the instruction)
-template <int OFF>
-__device__ __forceinline__ v4i ds_read_b128_at(uint32_t a) {
-    v4i v;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-    return v;
-}
-template <int OFF>
-__device__ __forceinline__ v2u ds_read_b64_at(uint32_t a) {
-    v2u v;
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-    return v;
-}
-template <int OFF>
-__device__ __forceinline__ uint32_t ds_read_u16_at(uint32_t a) {
-    uint32_t v;
-    asm volatile("ds_read_u16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-    return v;
-}
-
-// s_waitcnt vmcnt(BASE + k) for a wave-uniform runtime k (immediates only); vmcnt(0) past 7
-template <int BASE>
-__device__ __forceinline__ void wait_vm_plus(int k) {
-#define FQ_WAIT_PLUS(j)                                                           \
-    if (k == (j) && BASE + (j) <= 63) {                                           \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(BASE + (j) <= 63 ? BASE + (j) : 0) : "memory"); \
-        return;                                                                   \
-    }
-    FQ_WAIT_PLUS(0) FQ_WAIT_PLUS(1) FQ_WAIT_PLUS(2) FQ_WAIT_PLUS(3) FQ_WAIT_PLUS(4) FQ_WAIT_PLUS(5)
-    FQ_WAIT_PLUS(6) FQ_WAIT_PLUS(7)
-#undef FQ_WAIT_PLUS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int U, int D>
-__device__ __forceinline__ void wait_ring(int later) {
-    // s_waitcnt takes an immediate: `later` (< D) blocks of U DMA instructions may stay in flight
-#define FQ_WAIT_CASE(k)                                                                 \
-    if constexpr (D > (k)) {                                                            \
-        if (later == (k)) {                                                             \
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"((k) * U) : "memory");              \
-            return;                                                                     \
-        }                                                                               \
-    }
-    FQ_WAIT_CASE(11) FQ_WAIT_CASE(10) FQ_WAIT_CASE(9) FQ_WAIT_CASE(8) FQ_WAIT_CASE(7) FQ_WAIT_CASE(6)
-    FQ_WAIT_CASE(5) FQ_WAIT_CASE(4) FQ_WAIT_CASE(3) FQ_WAIT_CASE(2) FQ_WAIT_CASE(1)
-#undef FQ_WAIT_CASE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// Activation rows in LDS are 128 B (one group) with their eight 16-byte chunks XOR-swizzled by
-// (row & 7): the A-operand read (16 rows x 16 B per k-chunk) is then conflict-free per 8 lanes.
-__host__ __device__ inline int xswz(int row, int chunk) { return (chunk ^ (row & 7)) * 16; }
+#include "fq_lds.h"
 
 // =============================================================================================
 // Decode / small-M kernel (M <= 32): HBM-bound weight streaming.
@@ -121,7 +39,6 @@ __host__ __device__ inline int xswz(int row, int chunk) { return (chunk ^ (row &
 //     tile sums the S slabs in z order (sc1 loads, 8 in flight).  Deterministic: fixed order,
 //     no float atomics.  (MI355X_MICROARCH.md "Valid forms", row 1.)
 // =============================================================================================
-constexpr int FQ_BLOCK = 1536;  // bytes of one (16-column tile, group) fq6 block
 
 // waves per WG (one WG per CU): 8, or 4 for 32-row tiles (their reduction buffers are larger)
 #ifndef FQ_DECODE_WAVES
@@ -161,16 +78,11 @@ template <int MT, int XS, int SS> struct DecodeCfg {
     static constexpr int D = decode_depth_for(MT, XS, SLOT, U);   // ring depth
 };
 
-__host__ __device__ inline int decode_xsr(int MT) { return MT <= 16 ? 16 : 32; }
 __host__ __device__ inline int decode_slot(int MT, int XS, int SS) {
     const int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;
     return SS ? FQ_BLOCK + XP * 1024 + 64 + decode_xsr(MT) * 4 : FQ_BLOCK + XP * 1024;
 }
 
-// staged regions, rounded up to whole DMA instructions (each writes 64 lanes' worth)
-__host__ __device__ inline int decode_wsst_bytes(int nb) { return ((nb + 31) / 32) * 1024; }
-__host__ __device__ inline int decode_xsst_bytes(int ng, int MT) { return ((ng * decode_xsr(MT) + 63) / 64) * 256; }
-__host__ __device__ inline int decode_xst_bytes(int ng, int M) { return ((ng * M + 7) / 8) * 1024; }
 // fused quantizer: fp16 window of xwin (group, row) pairs (a multiple of 4, at most 32 = 8 KiB)
 __host__ __device__ inline int decode_xwin_bytes(int ng, int M, int xwin) { return (ng * M < xwin ? (ng * M + 3) / 4 * 4 : xwin) * 256; }
 // per-wave LDS: [ring D x SLOT][ws: nb x 8 dwords][xs: ng x XSR dwords][x: ng x M x 128 B]
