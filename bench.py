@@ -8,16 +8,15 @@ down 4096x11008), each = dynamic activation quantization + GEMM + dequant.  The 
 dependency chain as in decoding (each reads the previous one's output).  gate and up share their
 input, so by default they run as one linear over the concatenated weight image [gate; up]
 (22016x4096, output [gate | up], per-column arithmetic unchanged): 4 linears per layer
-(--no-merge: 5).  Default mode on one GPU (M <= 4): the whole step is ONE persistent launch
-(ops.LinearSeq / fq_linear_seq_run, fq_seq.hip) captured in a HIP graph; --mode launches: one
-fq_linear_w6ax launch per linear in a HIP graph (the JSON reports both on one GPU).
+(--no-merge: 5), one fq_linear_w6ax launch each (at decode sizes a single fused quantize+GEMM
+launch), the whole step captured into one HIP graph.
 
 Multi-GPU (torchrun, one process per GPU, RCCL): column-parallel N-shard of every linear, each
 rank packs and streams only its N/P rows, then ONE all-gather per linear of the dequantized
 fp16 output over xGMI.  Total work is fixed, so "scaling" is "strong".
 
-Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the chain
-launch, or the decode linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
+Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
+linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
 forward, timed on a bounded sample on this host).
 """
 import argparse
@@ -124,12 +123,6 @@ def run_step(stack, M, world, group=None, gather=True):
             dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
 
 
-def make_seq(stack):
-    """The whole step as ONE persistent launch (ops.LinearSeq, fq_linear_seq_*): the same
-    linears, the same data flow, dependencies derived from the buffers."""
-    return ops.LinearSeq([(p["x"], p["pk"], p["Nl"], p["abits"], p["out"]) for _, p in linears(stack)])
-
-
 def capture(fn, stream):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=stream):
@@ -184,14 +177,14 @@ def fp16_compare(shapes, M, abits, dev, reps=20):
     return out
 
 
-def pmc_traffic(config, merge, mode):
+def pmc_traffic(config, merge):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 FETCH_SIZE
     pass for this workload (profiles/rNN_pmc_summary.json, written by tools/pmc_summary.py, with
     the gfx950 x2 correction applied).  None when no pass matches."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), reverse=True):
         d = json.load(open(path))
-        if d.get("config") == config and d.get("merged_gate_up", False) == merge and d.get("mode", "launches") == mode:
+        if d.get("config") == config and d.get("merged_gate_up", False) == merge:
             return d["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
@@ -275,9 +268,6 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
-    ap.add_argument("--mode", choices=["seq", "launches"], default=None,
-                    help="seq: the whole step as one persistent chain launch (default for one GPU, M <= 4); "
-                         "launches: one launch per linear (+ an RCCL all-gather each when world > 1)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -293,18 +283,12 @@ def main():
     layers, M, lins, desc = cfg
     merge = not a.no_merge
     launch_lins = launch_list(lins, merge)
-    mode = a.mode or ("seq" if world == 1 and M <= 4 else "launches")
-    assert mode == "launches" or (world == 1 and M <= 4), "--mode seq: one GPU, M <= 4"
     stack = build_stack(cfg, rank, world, dev, merge)
-    seq = make_seq(stack) if mode == "seq" else None
     stream = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
 
     def step(gather=True):
-        if seq is not None:
-            seq.run()
-        else:
-            run_step(stack, M, world, gather=gather)
+        run_step(stack, M, world, gather=gather)
 
     # warm the per-stream workspace and RCCL communicators eagerly, on the capture stream
     with torch.cuda.stream(stream):
@@ -352,16 +336,14 @@ def main():
         elapsed = float(t.item())
     last = linears(stack)[-1][1]["out"]
     finite = bool(torch.isfinite(last.float()).all().item())
-    if seq is not None:
-        assert seq.error_word() == 0, "a dependency wait of the chain gave up"
 
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
     value = flops_step * a.steps / elapsed / 1e12
     tok_s = M * a.steps / elapsed
 
-    # roofline of the dominant kernel: a graph of the step's launches without the all-gathers
-    # (seq: the one chain launch; launches: the linears), timed with HIP events on its stream
-    fused = {(N, K): seq is not None or ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in launch_lins}
+    # roofline of the dominant kernel (the decode linear): a graph of the step's linear launches
+    # without the all-gathers, timed with HIP events on its stream
+    fused = {(N, K): ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in launch_lins}
     step_bytes = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins)
 
     def graph_time(fn, launches):
@@ -374,16 +356,10 @@ def main():
         return t, t / (a.roofline_reps * launches)
 
     n_lin = layers * len(launch_lins)
-    t_g, per_launch_s = graph_time(lambda: step(gather=False), 1 if seq is not None else n_lin)
-    bytes_launch = step_bytes / (1 if seq is not None else n_lin)
+    t_g, per_launch_s = graph_time(lambda: step(gather=False), n_lin)
+    bytes_launch = step_bytes / n_lin
     achieved = bytes_launch / per_launch_s / 1e9
-    per_linear = None
-    if seq is not None:  # the same step as one launch per linear, for comparison
-        _, pl = graph_time(lambda: run_step(stack, M, world, gather=False), n_lin)
-        per_linear = {"per_launch_us": round(pl * 1e6, 3), "ms_per_step": round(pl * n_lin * 1e3, 4),
-                      "achieved_GBps": round(step_bytes / n_lin / pl / 1e9, 1),
-                      "frac": round(step_bytes / n_lin / pl / 1e9 / HBM_PEAK_GBS, 4)}
-    traffic, traffic_src = pmc_traffic(a.config, merge, mode) if world == 1 else (None, None)
+    traffic, traffic_src = pmc_traffic(a.config, merge) if world == 1 else (None, None)
     if world > 1:  # the same step without the all-gathers (max over ranks)
         tg = torch.tensor([t_g / a.roofline_reps], dtype=torch.float64, device=dev)
         dist.all_reduce(tg, op=dist.ReduceOp.MAX)
@@ -407,7 +383,6 @@ def main():
         "tok_per_s": round(tok_s, 2),
         "config": {
             "workload": desc + ", dependent linear stack of every decoder layer per step",
-            "mode": mode,
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
             "parallelism": f"tp{world} column-parallel + RCCL all-gather per linear" if world > 1 else "single GPU",
@@ -415,8 +390,7 @@ def main():
             "launches_per_layer": [[name, N, K, ab] for (name, N, K, ab) in launch_lins],
         },
         "roofline": {
-            "kernel": ("fq_seq_kernel (the whole step: one launch)" if seq is not None else
-                       "fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else
+            "kernel": ("fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else
                        "fq_gemm_decode_kernel (+ quantize where unfused)"),
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -429,11 +403,9 @@ def main():
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
             "fused_launches": all(fused.values()),
-            "method": "graph of the step's launches only (no all-gather), HIP events on the capture stream",
+            "method": "graph of the step's linear launches only (no all-gather), HIP events on the capture stream",
         },
     }
-    if per_linear is not None:
-        res["roofline"]["one_launch_per_linear"] = per_linear
     if world > 1:
         res["gemm_only_ms_per_step"] = round(gemm_only_ms, 4)
         res["allgather_bytes_per_step_per_rank"] = int(layers * sum(2 * M * (N // world) * (world - 1)

@@ -54,11 +54,6 @@ _SIGS = {
     "fq_import_ref_w": ([P, P, I, I, P, P], I),
     "fq_import_ref_x": ([P, P, I, I, I, P, P, P], I),
     "fq_bmma_scratch_bytes": ([I, I, I], SZ),
-    "fq_linear_seq_workspace_bytes": ([I], SZ),
-    "fq_linear_seq_host_scratch_bytes": ([I], SZ),
-    "fq_linear_seq_error_offset": ([I], SZ),
-    "fq_linear_seq_prepare": ([P, I, I, P, SZ, P, P, P], I),
-    "fq_linear_seq_run": ([P, P], I),
 }
 EXPORTED = tuple(_SIGS) + ("fq_bmma_init", "fq_bmma_exec")
 

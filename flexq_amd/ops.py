@@ -186,79 +186,6 @@ def act_scratch_bytes(M, N, K):
     return int(_lib.load().fq_linear_act_scratch_bytes(M, N, K))
 
 
-# ------------------------------------------------------------------------- linear chains
-
-class _SeqDesc(ctypes.Structure):  # fq_linear_desc
-    _fields_ = [("x", ctypes.c_void_p), ("w_packed", ctypes.c_void_p), ("d", ctypes.c_void_p),
-                ("N", ctypes.c_int), ("K", ctypes.c_int), ("ldx", ctypes.c_int), ("abits", ctypes.c_int)]
-
-
-class _SeqPlan(ctypes.Structure):  # fq_linear_seq
-    _fields_ = [(f, ctypes.c_int) for f in ("count", "M", "grid", "slots", "wave_lds", "wsst", "xsst",
-                                             "redoff", "lds_bytes")] + [("workspace", ctypes.c_void_p)]
-
-
-class LinearSeq:
-    """A chain of decode linears run as ONE persistent launch (fq_linear_seq_*, include/flexq_hip.h).
-
-    entries: (x, w_packed, N, abits, out) per linear, in execution order.  x is fp16 [M, K] with a
-    contiguous last dimension (any row stride, e.g. a column slice of an earlier output), out is
-    fp16 [M, N] contiguous.  Linears whose buffers overlap an earlier linear's run after it (the
-    library derives the order from the byte ranges), so `run()` computes exactly what calling
-    linear_w6ax on each entry in order computes.  The tensors are referenced, not copied: the
-    chain reads and writes them in place on every run().  1 <= M <= 4, N % 4 == 0.
-    """
-
-    def __init__(self, entries):
-        _need(len(entries) > 0, "empty chain")
-        self._keep = []
-        descs = (_SeqDesc * len(entries))()
-        M = None
-        dev = None
-        for i, (x, wpk, N, abits, out) in enumerate(entries):
-            _need(isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float16 and x.dim() == 2,
-                  f"entry {i}: x must be a 2-D fp16 HIP tensor")
-            _need(x.stride(1) == 1, f"entry {i}: x rows must be contiguous")
-            Mi, K = x.shape
-            M = Mi if M is None else M
-            dev = x.device if dev is None else dev
-            _need(Mi == M, f"entry {i}: every linear of a chain has the same M")
-            _k_ok(K)
-            _img_ok(wpk, N, K)
-            _dev(out, torch.float16, f"entry {i}: out", 2)
-            _need(tuple(out.shape) == (M, N), f"entry {i}: out must be [M, N] = {(M, N)}")
-            _need(abits in (6, 8), "abits must be 6 or 8")
-            for t in (wpk, out):
-                _need(t.device == dev, "all tensors of a chain must be on one device")
-            descs[i] = _SeqDesc(x.data_ptr(), wpk.data_ptr(), out.data_ptr(), N, K,
-                                x.stride(0) if M > 1 else K, abits)
-            self._keep += [x, wpk, out]
-        lib = _lib.load()
-        n = len(entries)
-        self.count, self.M, self.device = n, M, dev
-        self._ws = torch.empty(int(lib.fq_linear_seq_workspace_bytes(n)), dtype=torch.uint8, device=dev)
-        self._host = ctypes.create_string_buffer(int(lib.fq_linear_seq_host_scratch_bytes(n)))
-        self._descs = descs
-        self.plan = _SeqPlan()
-        s = _stream(self._ws)
-        _lib.call("fq_linear_seq_prepare", ctypes.cast(descs, ctypes.c_void_p), n, M, _ptr(self._ws),
-                  ctypes.c_size_t(self._ws.numel()), ctypes.byref(self.plan), ctypes.cast(self._host, ctypes.c_void_p), s)
-        torch.cuda.current_stream(dev).synchronize()  # the host descriptor image is no longer needed
-        self._err_off = int(lib.fq_linear_seq_error_offset(n))
-
-    def run(self):
-        """One launch of the whole chain on torch's current stream (graph-capturable)."""
-        _lib.call("fq_linear_seq_run", ctypes.byref(self.plan), _stream(self._ws))
-
-    def error_word(self):
-        """Non-zero if a dependency wait gave up (synchronises)."""
-        return int(self._ws[self._err_off:self._err_off + 4].view(torch.int32).item())
-
-    def counters(self):
-        """The per-workgroup progress flags (all zero between runs; synchronises)."""
-        return self._ws[:4 * self.plan.grid].view(torch.int32).cpu()
-
-
 # ------------------------------------------------------------------------- reference layouts
 
 def _rows_ok(R):

@@ -111,40 +111,6 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
                          uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                          size_t workspace_bytes, fq_stream_t stream);
 
-/* ---- a chain of decode linears in ONE launch ------------------------------------------------ */
-/* Replaces a sequence of FLEXQGEMMWrapper::gemm(const half* A ...) calls issued back to back on one
- * stream (flexq_gemm_wrapper.cu:99-122; FT issues them per layer, FfnLayer.cc:371-401,521-561).
- * Each linear j: d_j[M][N] = fq_linear_w6ax(x_j[M][K] (row stride ldx), w_j) with the fused decode
- * arithmetic (the same bits as fq_linear_w6ax when its plan has no k-split).  Linear j starts
- * reading x_j / writing d_j only after every earlier linear whose byte ranges it overlaps (RAW,
- * WAR, WAW) is complete, so the chain computes what the launches in order compute; an output of
- * one linear may be (part of) the input of a later one.  Limits: 1 <= M <= 4, N % 4 == 0,
- * K % 128 == 0, ldx >= K, ldx % 8 == 0, x 16-byte and d 8-byte aligned.
- * prepare (offline, once): validates, plans, and enqueues the upload of the descriptors (from
- * host_scratch, fq_linear_seq_host_scratch_bytes(count) bytes the caller keeps valid until the
- * stream has run the copy) and the zeroing of the counters into `workspace`
- * (fq_linear_seq_workspace_bytes(count) bytes, 16-byte aligned, device).  run: one launch,
- * graph-capturable; leaves the counters zeroed.  The uint32 at workspace +
- * fq_linear_seq_error_offset(count) becomes non-zero if a dependency wait gave up (a co-resident
- * grid is assumed: one workgroup per CU, nothing else running on the device). */
-typedef struct fq_linear_desc {
-    const uint16_t *x;    /* fp16 [M][ldx] */
-    const void *w_packed; /* weight image of an [N][K] matrix */
-    uint16_t *d;          /* fp16 [M][N] */
-    int N, K, ldx, abits;
-} fq_linear_desc;
-typedef struct fq_linear_seq {
-    int count, M, grid, slots, wave_lds, wsst, xsst, redoff, lds_bytes;
-    void *workspace;
-} fq_linear_seq;
-size_t fq_linear_seq_workspace_bytes(int count);
-size_t fq_linear_seq_host_scratch_bytes(int count);
-size_t fq_linear_seq_error_offset(int count);
-fq_status fq_linear_seq_prepare(const fq_linear_desc *lin, int count, int M, void *workspace,
-                                size_t workspace_bytes, fq_linear_seq *plan, void *host_scratch,
-                                fq_stream_t stream);
-fq_status fq_linear_seq_run(const fq_linear_seq *plan, fq_stream_t stream);
-
 /* ---- reference-layout entry points (drop-in for FlexQ's own formats) ------------------------ */
 /* flexq_bit_packing(const int* in, int* out, M, K, BIT, stream) (engine/src/pack/bit_packing.h:34,
  * bit_packing.cu:147-156): raw b-bit patterns [M][K] -> bit planes int32
