@@ -114,7 +114,12 @@ template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0>
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int M, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
-    float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin) {
+    float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir) {
+    // Every kernel argument is needed before the first DMA: make the compiler load them all in
+    // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
+    // second serial round trip before the first DMA; tools/stamps.py).
+    asm volatile("" ::"s"(xq), "s"(xs), "s"(xh), "s"(abits), "s"(wpk), "s"(M), "s"(N), "s"(K), "s"(d), "s"(slabs),
+                 "s"(tickets), "s"(S), "s"(IPW), "s"(RC), "s"(xwin), "s"(iq), "s"(ir), "s"(gridDim.x));
     using C = DecodeCfg<MT, XS, SS>;
     constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
     static_assert(!FUSE || (XS == 0 && SS == 0), "fused quantization stages into LDS");
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     // cost microseconds of scalar code before the first DMA).  The grid is a multiple of S, so a
     // WG's k-split z is fixed and its items' tiles are t0, t0 + tstep, ...
     const int bid = blockIdx.x, grid = gridDim.x;
-    const int nit = (unsigned)(items - bid + grid - 1) / (unsigned)grid;  // >= 1
+    const int nit = iq + (bid < ir ? 1 : 0);  // items for this WG (>= 1): host-computed quotient
     const int z = S == 1 ? 0 : (unsigned)bid % (unsigned)S;
     const int t0 = S == 1 ? bid : (unsigned)bid / (unsigned)S, tstep = S == 1 ? grid : (unsigned)grid / (unsigned)S;
     const int gz0 = S == 1 ? 0 : (unsigned)(z * G) / (unsigned)S;
@@ -712,6 +717,7 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
 // =============================================================================================
 struct DecodePlan {
     int MT, S, grid, IPW, RC, XS, SS, xwin;  // xwin: fused fp16 window (0 = not fused)
+    int NT;                                  // 16-column tiles
     int cost4;                               // modelled time, quarter-blocks per wave (see decode_plan)
     bool fits;
 };
@@ -750,6 +756,7 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused) {
     DecodePlan p;
     p.MT = M <= 4 ? 4 : (M <= 8 ? 8 : (M <= 16 ? 16 : 32));
     const int NT = (N + 15) / 16, G = K / FQ_GROUP;
+    p.NT = NT;
     const int cus = device_cus();
     const int NW = decode_waves(p.MT);
     // k-split S minimises the modelled GEMM cost; S divides the grid so that z = blockIdx % S is
@@ -849,7 +856,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
     if (abl == v) {                                                                                           \
         hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
                            a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
-                           slabs, tickets, p.S, p.IPW, p.RC, p.xwin);                                         \
+                           slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / p.grid, p.NT * p.S % p.grid); \
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
@@ -859,7 +866,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 #endif
     hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG>), grid, block, lds, stream, a.xq, a.xs, a.xh,
                        a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S, p.IPW,
-                       p.RC, p.xwin);
+                       p.RC, p.xwin, p.NT * p.S / p.grid, p.NT * p.S % p.grid);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }

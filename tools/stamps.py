@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "tools", "libflexq_hip_abl.so")
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [(12288, 4096), (4096, 4096), (11008, 4096), (4096, 11008), (28672, 8192), (8192, 28672)]
