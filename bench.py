@@ -321,10 +321,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
+        ev0.record(stream)  # HIP events on the launch stream, bracketing exactly the timed steps
         for _ in range(a.steps):
             replay()
+        ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -356,7 +359,11 @@ def main():
         return t, t / (a.roofline_reps * launches)
 
     n_lin = layers * len(launch_lins)
-    t_g, per_launch_s = graph_time(lambda: step(gather=False), n_lin)
+    if world == 1:  # the timed region itself: only the linear launches run in it
+        t_g = ev0.elapsed_time(ev1) / 1e3 * a.roofline_reps / a.steps
+        per_launch_s = ev0.elapsed_time(ev1) / 1e3 / (a.steps * n_lin)
+    else:  # without the all-gathers
+        t_g, per_launch_s = graph_time(lambda: step(gather=False), n_lin)
     bytes_launch = step_bytes / n_lin
     achieved = bytes_launch / per_launch_s / 1e9
     traffic, traffic_src = pmc_traffic(a.config, merge) if world == 1 else (None, None)
@@ -403,7 +410,9 @@ def main():
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
             "fused_launches": all(fused.values()),
-            "method": "graph of the step's linear launches only (no all-gather), HIP events on the capture stream",
+            "method": ("HIP events on the launch stream around the timed steps (only the linear launches run)"
+                       if world == 1 else "graph of the step's linear launches only (no all-gather), HIP events "
+                                          "on the capture stream"),
         },
     }
     if world > 1:

@@ -54,6 +54,8 @@ _SIGS = {
     "fq_import_ref_w": ([P, P, I, I, P, P], I),
     "fq_import_ref_x": ([P, P, I, I, I, P, P, P], I),
     "fq_bmma_scratch_bytes": ([I, I, I], SZ),
+    "fq_rmsnorm_quantize": ([P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),
+    "fq_silu_mul_quantize": ([P, P, I, I, I, I, P, P, P, P], I),
 }
 EXPORTED = tuple(_SIGS) + ("fq_bmma_init", "fq_bmma_exec")
 

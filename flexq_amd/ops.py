@@ -186,6 +186,56 @@ def act_scratch_bytes(M, N, K):
     return int(_lib.load().fq_linear_act_scratch_bytes(M, N, K))
 
 
+# ------------------------------------------------------------------------- fused producers
+
+def rmsnorm_quantize(residual, gamma, abits, eps=1e-6, input=None, return_normed=False):
+    """Residual add + RMSNorm + dynamic group quantization (fq_rmsnorm_quantize; the reference's
+    generalAddResidualT5LayerNormFlexQFusion, layernorm_kernels.cu:1851-2051).  residual fp16
+    [M,K] is updated IN PLACE to residual + input when input is given.  Returns (xq int8 [M,K],
+    xs fp16 [K/128, M]) (+ the fp16 normalised activations)."""
+    _dev(residual, torch.float16, "residual", 2)
+    M, K = residual.shape
+    _k_ok(K)
+    _need(K <= 32768, "K must be <= 32768")
+    _dev(gamma, torch.float16, "gamma", 1)
+    _need(gamma.numel() == K and gamma.device == residual.device, "gamma must be [K] on the residual's device")
+    if input is not None:
+        _dev(input, torch.float16, "input", 2)
+        _need(tuple(input.shape) == (M, K) and input.device == residual.device, "input must match residual")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    dev = residual.device
+    xq = torch.empty((M, K), dtype=torch.int8, device=dev)
+    xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=dev)
+    normed = torch.empty((M, K), dtype=torch.float16, device=dev) if return_normed else None
+    _lib.call("fq_rmsnorm_quantize", _ptr(input), _ptr(residual), _ptr(gamma), ctypes.c_float(eps), M, K, abits,
+              _ptr(xq), _ptr(xs), _ptr(normed), _stream(residual))
+    return (xq, xs, normed) if return_normed else (xq, xs)
+
+
+def silu_mul_quantize(gate, up, abits, return_act=False):
+    """SiLU(gate) * up + dynamic group quantization (fq_silu_mul_quantize; the reference's
+    flexq_generic_activation, activation_kernels.cu:245-450).  gate and up are fp16 [M,N] views
+    with a contiguous last dimension and one common row stride (e.g. the two column halves of a
+    merged gate_up output).  Returns (xq int8 [M,N], xs fp16 [N/128, M]) (+ the fp16 product)."""
+    for name, t in (("gate", gate), ("up", up)):
+        _need(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float16 and t.dim() == 2,
+              f"{name} must be a 2-D fp16 HIP tensor")
+        _need(t.stride(1) == 1, f"{name} rows must be contiguous")
+    _need(gate.shape == up.shape and gate.stride(0) == up.stride(0) and gate.device == up.device,
+          "gate and up must have one shape, row stride and device")
+    M, N = gate.shape
+    _k_ok(N)
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    ld = gate.stride(0) if M > 1 else N
+    dev = gate.device
+    xq = torch.empty((M, N), dtype=torch.int8, device=dev)
+    xs = torch.empty((N // GROUP, M), dtype=torch.float16, device=dev)
+    act = torch.empty((M, N), dtype=torch.float16, device=dev) if return_act else None
+    _lib.call("fq_silu_mul_quantize", _ptr(gate), _ptr(up), ld, M, N, abits, _ptr(xq), _ptr(xs), _ptr(act),
+              _stream(gate))
+    return (xq, xs, act) if return_act else (xq, xs)
+
+
 # ------------------------------------------------------------------------- reference layouts
 
 def _rows_ok(R):

@@ -111,6 +111,30 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
                          uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                          size_t workspace_bytes, fq_stream_t stream);
 
+/* ---- fused producers of the activation codes ---------------------------- */
+/* Residual add + RMSNorm (T5 / LLaMA style: no mean, no bias) + dynamic group quantization, one
+ * launch.  Replaces generalAddResidualT5LayerNormFlexQFusion / invokeGeneralAddResidualT5PreLayerNorm
+ * (e2e .../kernels/layernorm_kernels.cu:1851-2106) with this engine's activation format:
+ *   residual[m][k] = half_clamp(float(input[m][k]) + float(residual[m][k]))   (in place; input
+ *                    may be NULL: no add, the residual is only read)
+ *   normed[m][k]   = half_clamp((float(residual[m][k]) * rs[m]) * float(gamma[k])),
+ *                    rs[m] = 1 / sqrt(sum_k float(residual[m][k])^2 / K + eps)
+ *   xq, xs         = fq_quantize_act(normed, abits)     (bit-identical codes and scales)
+ * half_clamp = the reference's clamp_inf_for_half (+-64504, then fp16).  normed_out (fp16
+ * [M][K]) is optional.  K % 128 == 0, K <= 32768, 16-byte aligned rows. */
+fq_status fq_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const uint16_t *gamma,
+                              float eps, int M, int K, int abits, int8_t *xq, uint16_t *xs,
+                              uint16_t *normed_out, fq_stream_t stream);
+/* SiLU(gate) * up + dynamic group quantization, one launch.  Replaces flexq_generic_activation
+ * (e2e .../kernels/activation_kernels.cu:245-450, launch :556-590; A8 for down_proj,
+ * FfnLayer.cc:67-77):  act[m][n] = half(silu(float(gate[m][n])) * float(up[m][n])),
+ * silu(v) = v / (1 + exp(-v)); gate and up rows have stride ld (elements), e.g. the two halves of
+ * a merged [gate | up] output with ld = 2N.  xq int8 [M][N], xs fp16 [N/128][M], act_out
+ * (fp16 [M][N]) optional.  N % 128 == 0, 16-byte aligned rows. */
+fq_status fq_silu_mul_quantize(const uint16_t *gate, const uint16_t *up, int ld, int M, int N,
+                               int abits, int8_t *xq, uint16_t *xs, uint16_t *act_out,
+                               fq_stream_t stream);
+
 /* ---- reference-layout entry points (drop-in for FlexQ's own formats) ------------------------ */
 /* flexq_bit_packing(const int* in, int* out, M, K, BIT, stream) (engine/src/pack/bit_packing.h:34,
  * bit_packing.cu:147-156): raw b-bit patterns [M][K] -> bit planes int32

@@ -16,6 +16,10 @@
  *                          double and rounded once to fp16.
  *   fqo_pack_fq6 / fqo_unpack_fq6   this build's own 6-bit weight image --
  *                          a model of the HIP packer, not a reference function.
+ *   fqo_rmsnorm_quantize   e2e/src/fastertransformer/kernels/layernorm_kernels.cu:1851-2051
+ *                          (residual + RMSNorm + quantize; the HIP kernel's summation order)
+ *   fqo_silu_mul_ref       e2e/src/fastertransformer/kernels/activation_kernels.cu:133,245-450
+ *                          (SiLU(gate) * up, double precision: a tolerance reference)
  *
  * Parity pinning: the reference ships no kernel golden vectors (inputs are time-seeded,
  * test_bgemm_kernel.cu:178).  The kernel-side functions are pinned by (1) the packing KAT of
@@ -387,4 +391,79 @@ long fqo_check_div_by_const(int hi) {
         if (b0 != b1) bad++;
     }
     return bad;
+}
+
+/* ---------------------------------------------------------------- fused producers (§8(f)1) */
+
+/* clamp_inf_for_half (e2e .../kernels/reduce_kernel_utils.cuh:357-361): +-(65504 - 1000), then fp16 */
+static uint16_t half_clamp(float v) {
+    const float c = v > 0.0f ? fminf(v, 65504.0f - 1000.0f) : fmaxf(v, -65504.0f + 1000.0f);
+    return fqo_f32_to_f16(c);
+}
+
+/* Residual add + RMSNorm + quantization, restating generalAddResidualT5LayerNormFlexQFusion
+ * (e2e .../kernels/layernorm_kernels.cu:1851-2051) with the arithmetic order of this build's
+ * kernel (flexq_amd/csrc/fq_producers.hip), so that the comparison is bit-exact:
+ *   r = half_clamp(float(in) + float(res))                                  (:1883)
+ *   ss: thread t of T sums fmaf(v, v, acc) over its chunks c*T+t of 8 values in order; a 64-lane
+ *       xor butterfly (32, 16, ..., 1); the T/64 waves added in order.  T = 256, 512 or 1024 as
+ *       the row has <= 256, <= 512 or more chunks (the kernel's workgroup size)
+ *   rs = 1 / sqrt(ss / K + eps)        (the reference: rsqrtf, :1890)
+ *   normed = half_clamp((float(r) * rs) * float(gamma))                     (:1898)
+ *   codes/scales = fqo_quantize_engine(normed)   (the reference quantizes with the same rule, :1932-1990)
+ * input may be NULL (no residual add).  residual is updated in place. */
+int fqo_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const uint16_t *gamma, float eps,
+                         int M, int K, int bits, int8_t *xq, uint16_t *xs, uint16_t *normed) {
+    if (M <= 0 || K <= 0 || K % 128 || (bits != 6 && bits != 8)) return 1;
+    const int nq = K / 8, T = nq <= 256 ? 256 : nq <= 512 ? 512 : 1024;
+    float *acc = (float *)malloc(sizeof(float) * T);
+    if (!acc) return 2;
+    for (int m = 0; m < M; m++) {
+        uint16_t *res = residual + (size_t)m * K;
+        for (int t = 0; t < T; t++) acc[t] = 0.0f;
+        for (int c = 0; c * T < nq; c++)
+            for (int t = 0; t < T; t++) {
+                const int q = c * T + t;
+                if (q >= nq) continue;
+                for (int e = 0; e < 8; e++) {
+                    const size_t k = 8 * (size_t)q + e;
+                    if (input) res[k] = half_clamp(f16_to_f32(input[(size_t)m * K + k]) + f16_to_f32(res[k]));
+                    const float v = f16_to_f32(res[k]);
+                    acc[t] = fmaf(v, v, acc[t]);
+                }
+            }
+        float wsum[16];
+        for (int w = 0; w < T / 64; w++) {
+            float lane[64];
+            for (int l = 0; l < 64; l++) lane[l] = acc[64 * w + l];
+            for (int off = 32; off >= 1; off >>= 1) {
+                float nxt[64];
+                for (int l = 0; l < 64; l++) nxt[l] = lane[l] + lane[l ^ off];
+                memcpy(lane, nxt, sizeof(lane));
+            }
+            wsum[w] = lane[0];
+        }
+        float ss = wsum[0];
+        for (int w = 1; w < T / 64; w++) ss = ss + wsum[w];
+        const float rs = 1.0f / sqrtf(ss / (float)K + eps);
+        for (int k = 0; k < K; k++) {
+            const float p = f16_to_f32(res[k]) * rs;
+            normed[(size_t)m * K + k] = half_clamp(p * f16_to_f32(gamma[k]));
+        }
+    }
+    free(acc);
+    return fqo_quantize_engine(normed, M, K, bits, xq, xs);
+}
+
+/* SiLU(gate) * up in double precision, rounded once to fp16 (the tolerance reference of
+ * flexq_generic_activation, e2e .../kernels/activation_kernels.cu:133,300; the kernels compute
+ * it in fp32 with a fast exp, so they may differ by one fp16 ulp). gate/up rows stride ld. */
+int fqo_silu_mul_ref(const uint16_t *gate, const uint16_t *up, int ld, int M, int N, uint16_t *act) {
+    if (M <= 0 || N <= 0 || ld < N) return 1;
+    for (int m = 0; m < M; m++)
+        for (int n = 0; n < N; n++) {
+            const double g = f16_to_f32(gate[(size_t)m * ld + n]), u = f16_to_f32(up[(size_t)m * ld + n]);
+            act[(size_t)m * N + n] = fqo_f64_to_f16(g / (1.0 + exp(-g)) * u);
+        }
+    return 0;
 }

@@ -44,6 +44,8 @@ def lib():
             "fqo_xs_to_ref_dup": [P, I, I, P],
             "fqo_pack_fq6": [P, P, I, I, P],
             "fqo_unpack_fq6": [P, I, I, P, P],
+            "fqo_rmsnorm_quantize": [P, P, P, ctypes.c_float, I, I, I, P, P, P],
+            "fqo_silu_mul_ref": [P, P, I, I, I, P],
         }.items():
             fn = getattr(L, name)
             fn.argtypes = args
@@ -99,6 +101,31 @@ def quantize_engine(x_f16, bits):
     xs = np.zeros((K // 128, M), dtype=np.float16)
     _check(lib().fqo_quantize_engine(_p(x), M, K, bits, _p(q), _p(xs)), "quantize_engine")
     return q, xs
+
+
+def rmsnorm_quantize(inp, residual, gamma, eps, bits):
+    """Residual add + RMSNorm + engine quantizer (layernorm_kernels.cu:1851-2051, the HIP kernel's
+    summation order) -> (residual_out, normed fp16 [M,K], q int8 [M,K], xs fp16 [K/128, M])."""
+    res = np.array(residual, dtype=np.float16, copy=True, order="C")
+    M, K = res.shape
+    g = np.ascontiguousarray(gamma, dtype=np.float16)
+    normed = np.zeros((M, K), dtype=np.float16)
+    q = np.zeros((M, K), dtype=np.int8)
+    xs = np.zeros((K // 128, M), dtype=np.float16)
+    inp = None if inp is None else np.ascontiguousarray(inp, dtype=np.float16)
+    _check(lib().fqo_rmsnorm_quantize(None if inp is None else _p(inp), _p(res), _p(g), eps, M, K, bits,
+                                      _p(q), _p(xs), _p(normed)), "rmsnorm_quantize")
+    return res, normed, q, xs
+
+
+def silu_mul_ref(gate, up):
+    """half(silu(gate) * up) evaluated in double (activation_kernels.cu:133,300)."""
+    g = np.ascontiguousarray(gate, dtype=np.float16)
+    u = np.ascontiguousarray(up, dtype=np.float16)
+    M, N = g.shape
+    act = np.zeros((M, N), dtype=np.float16)
+    _check(lib().fqo_silu_mul_ref(_p(g), _p(u), N, M, N, _p(act)), "silu_mul_ref")
+    return act
 
 
 def xs_to_ref_dup(xs, M, K):

@@ -1,0 +1,129 @@
+"""GPU parity tests of the fused activation producers through the C ABI.
+
+fq_rmsnorm_quantize (layernorm_kernels.cu:1851-2051): residual, normalised fp16 values, codes
+and scales bit-exact against oracle.rmsnorm_quantize, which restates the kernel's arithmetic
+order (IEEE add/mul/div/sqrt, a fixed reduction tree).
+
+fq_silu_mul_quantize (activation_kernels.cu:245-450): the fp16 product within one fp16 ulp of
+the double-precision oracle (the kernel uses fp32 and the hardware's fast exp, as the reference
+uses __expf); codes and scales bit-exact against the engine quantizer applied to the kernel's own
+fp16 product, i.e. the quantization step is exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from common import oracle, rng
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from flexq_amd import ops as _ops
+    return _ops
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def hbits(a):
+    return np.ascontiguousarray(a).view(np.uint16)
+
+
+@pytest.mark.parametrize("M,K", [(1, 4096), (3, 4096), (16, 11008), (5, 128), (2, 32768), (64, 8192), (7, 384),
+                                 (2048, 4096)])
+@pytest.mark.parametrize("bits", [6, 8])
+@pytest.mark.parametrize("with_input", [True, False])
+def test_rmsnorm_quantize_bit_exact(ops, dev, M, K, bits, with_input):
+    r = rng(M * 131 + K + bits + with_input)
+    res = (r.standard_normal((M, K)) * 2.0).astype(np.float16)
+    inp = (r.standard_normal((M, K)) * 0.5).astype(np.float16) if with_input else None
+    gamma = (1.0 + 0.2 * r.standard_normal(K)).astype(np.float16)
+    res[0, :7] = [0.0, -0.0, 6e-8, -3e4, 3e4, 1e-3, 65504.0]  # zeros, subnormal, clamp range
+    eps = 1e-5
+    res_d = to_dev(res, dev)
+    xq, xs, normed = ops.rmsnorm_quantize(res_d, to_dev(gamma, dev), bits, eps=eps,
+                                          input=None if inp is None else to_dev(inp, dev), return_normed=True)
+    r_ref, n_ref, q_ref, xs_ref = oracle.rmsnorm_quantize(inp, res, gamma, eps, bits)
+    np.testing.assert_array_equal(hbits(host(res_d)), hbits(r_ref), err_msg="residual")
+    np.testing.assert_array_equal(hbits(host(normed)), hbits(n_ref), err_msg="normed")
+    np.testing.assert_array_equal(host(xq), q_ref, err_msg="codes")
+    np.testing.assert_array_equal(hbits(host(xs)), hbits(xs_ref), err_msg="scales")
+
+
+def test_rmsnorm_zero_and_huge_rows(ops, dev):
+    """An all-zero row (scale 0 -> codes 0, the reference's NaN path defined) and a row of
+    near-fp16-max values."""
+    K = 1024
+    res = np.zeros((2, K), np.float16)
+    res[1] = 6.0e4
+    gamma = np.ones(K, np.float16)
+    xq, xs, normed = ops.rmsnorm_quantize(to_dev(res, dev), to_dev(gamma, dev), 6, return_normed=True)
+    _, n_ref, q_ref, xs_ref = oracle.rmsnorm_quantize(None, res, gamma, 1e-6, 6)
+    np.testing.assert_array_equal(hbits(host(normed)), hbits(n_ref))
+    np.testing.assert_array_equal(host(xq), q_ref)
+    np.testing.assert_array_equal(hbits(host(xs)), hbits(xs_ref))
+    assert not host(xq)[0].any()
+
+
+def within_one_ulp(got, ref):
+    g = got.astype(np.float64)
+    f = ref.astype(np.float64)
+    ulp = np.spacing(np.abs(ref).astype(np.float16)).astype(np.float64)
+    return np.abs(g - f) <= ulp
+
+
+@pytest.mark.parametrize("M,N", [(1, 11008), (16, 11008), (3, 128), (64, 14336), (5, 640), (2048, 14336)])
+@pytest.mark.parametrize("bits", [8, 6])
+def test_silu_mul_quantize(ops, dev, M, N, bits):
+    """gate and up as the two column halves of one merged gate_up output [M, 2N] (the layout of
+    bench.py's merged gate/up linear), row stride 2N."""
+    r = rng(M * 7 + N + bits)
+    gu = (r.standard_normal((M, 2 * N)) * 3.0).astype(np.float16)
+    gu[0, :4] = [0.0, -20.0, 20.0, -0.0]
+    gu_d = to_dev(gu, dev)
+    gate, up = gu_d[:, :N], gu_d[:, N:]
+    xq, xs, act = ops.silu_mul_quantize(gate, up, bits, return_act=True)
+    act_h = host(act)
+    ref = oracle.silu_mul_ref(gu[:, :N], gu[:, N:])
+    ok = within_one_ulp(act_h, ref)
+    assert ok.all(), f"{int((~ok).sum())} products more than one fp16 ulp off"
+    q_ref, xs_ref = oracle.quantize_engine(act_h, bits)
+    np.testing.assert_array_equal(host(xq), q_ref)
+    np.testing.assert_array_equal(hbits(host(xs)), hbits(xs_ref))
+
+
+def test_producer_feeds_gemm(ops, dev):
+    """SiLU * up -> A8 codes -> W6A8 down_proj GEMM equals quantize(act) -> GEMM, bit for bit."""
+    M, N, K = 4, 1024, 2048  # down_proj: K = the FFN width
+    r = rng(3)
+    gu = r.standard_normal((M, 2 * K)).astype(np.float16)
+    gu_d = to_dev(gu, dev)
+    xq, xs, act = ops.silu_mul_quantize(gu_d[:, :K], gu_d[:, K:], 8, return_act=True)
+    w = (r.standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    wpk, _ = ops.quantize_pack_w6(to_dev(w, dev))
+    d1 = ops.gemm_w6ax(xq, xs, wpk, N, 8)
+    xq2, xs2 = ops.quantize_act(act, 8)
+    d2 = ops.gemm_w6ax(xq2, xs2, wpk, N, 8)
+    np.testing.assert_array_equal(hbits(host(d1)), hbits(host(d2)))
+
+
+def test_producer_status_codes(ops, dev):
+    from flexq_amd import _lib
+    lib = _lib.load()
+    P = lambda n: torch.empty(n, dtype=torch.uint8, device=dev)  # noqa: E731
+    a, b, c = P(1 << 16), P(1 << 16), P(1 << 16)
+    s = ops._stream(a)
+    ptr = ops._ptr
+    assert lib.fq_rmsnorm_quantize(None, ptr(a), ptr(b), 1e-6, 1, 100, 6, ptr(c), ptr(c), None, s) == 2
+    assert lib.fq_rmsnorm_quantize(None, ptr(a), ptr(b), 1e-6, 1, 128, 7, ptr(c), ptr(c), None, s) == 3
+    assert lib.fq_rmsnorm_quantize(None, None, ptr(b), 1e-6, 1, 128, 6, ptr(c), ptr(c), None, s) == 1
+    assert lib.fq_silu_mul_quantize(ptr(a), ptr(b), 100, 1, 200, 8, ptr(c), ptr(c), None, s) == 2
+    assert lib.fq_silu_mul_quantize(ptr(a), ptr(b), 128, 1, 128, 5, ptr(c), ptr(c), None, s) == 3
