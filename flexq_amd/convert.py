@@ -1,0 +1,172 @@
+"""Offline weight converter and on-disk packed-weight format.
+
+The reference's serving path loads pre-packed 6-bit weights per tensor-parallel rank
+(`LlamaDecoderLayerWeight.cc:381-410`: `*.attention.query_key_value.weight.<rank>.bin`, ...), but
+the converter that writes them is not in the repository.  This module is that converter for this
+engine: fp16 HF weights -> per-(row, 128-group) symmetric 6-bit codes with the engine rounding
+rule (fq_quantize_pack_w6, the same rule as the activation quantizer) -> the weight image (codes
+in fq6 blocks + blocked fp16 scales) -> one `.fqw6` file per linear and rank.
+
+File layout (little-endian, 64-byte header, then the image exactly as the GEMM reads it):
+  0  magic  b"FQW6IMG\\0"           32 tp_rank  i32
+  8  version u32 (1)                36 tp_size  i32
+  12 header bytes u32 (64)          40 abits    i32 (activation bits this linear runs with)
+  16 N   i32 (rows in this file)    44 crc32    u32 of the image bytes
+  20 K   i32                        48 image bytes u64 (= fq_packed_w_bytes(N, K))
+  24 N_full i32                     56 reserved (8 bytes, zero)
+  28 row_offset i32 (first row of this shard in the rank-major gathered output = rank * N)
+
+Tensor parallelism follows flexq_amd.dist: every linear is column-parallel (rank p owns output
+rows [p N/P, (p+1) N/P), 16-row aligned).  Fused linears shard their parts separately and stack
+them per rank (qkv = [q_p; k_p; v_p], gate_up = [gate_p; up_p], as FT's per-rank
+`3 * hidden / tp` layout), so a rank's gate and up halves meet in its own output for
+fq_silu_mul_quantize.  down_proj runs W6A8 (`--flex_linear_quant`, int_llama_layer.py:35-37),
+the others W6A6.
+
+Conversion runs the HIP packer (a GPU is required); reading and writing files does not.
+"""
+import argparse
+import json
+import os
+import struct
+import zlib
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dist import shard_range
+
+MAGIC = b"FQW6IMG\0"
+VERSION = 1
+HEADER = 64
+_FMT = "<8sIIiiiiiiiIQ8x"  # 64 bytes
+assert struct.calcsize(_FMT) == HEADER
+
+
+def packed_bytes(N, K):
+    return int(_lib.load().fq_packed_w_bytes(N, K))
+
+
+def save_image(path, image, N, K, abits, N_full=None, row_offset=0, tp_rank=0, tp_size=1):
+    """Write one weight image (uint8 tensor of fq_packed_w_bytes(N, K) bytes) with its header."""
+    img = image.detach().to("cpu").contiguous().numpy().view(np.uint8).reshape(-1)
+    if img.size != packed_bytes(N, K):
+        raise ValueError(f"image has {img.size} bytes, expected {packed_bytes(N, K)} for N={N} K={K}")
+    if abits not in (6, 8):
+        raise ValueError("abits must be 6 or 8")
+    hdr = struct.pack(_FMT, MAGIC, VERSION, HEADER, N, K, N if N_full is None else N_full, row_offset,
+                      tp_rank, tp_size, abits, zlib.crc32(img) & 0xFFFFFFFF, img.size)
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(hdr)
+        f.write(img.tobytes())
+    os.replace(tmp, path)
+
+
+def read_header(path):
+    with open(path, "rb") as f:
+        raw = f.read(HEADER)
+    if len(raw) != HEADER:
+        raise ValueError(f"{path}: truncated header")
+    magic, ver, hb, N, K, N_full, off, rank, size, abits, crc, nbytes = struct.unpack(_FMT, raw)
+    if magic != MAGIC or ver != VERSION or hb != HEADER:
+        raise ValueError(f"{path}: not an fqw6 v{VERSION} file")
+    return dict(N=N, K=K, N_full=N_full, row_offset=off, tp_rank=rank, tp_size=size, abits=abits, crc32=crc,
+                image_bytes=nbytes)
+
+
+def load_image(path, device=None):
+    """-> (uint8 image tensor, header dict); checks the size and the CRC of the payload."""
+    meta = read_header(path)
+    if meta["image_bytes"] != packed_bytes(meta["N"], meta["K"]):
+        raise ValueError(f"{path}: image size does not match N={meta['N']} K={meta['K']}")
+    img = np.fromfile(path, dtype=np.uint8, offset=HEADER)
+    if img.size != meta["image_bytes"]:
+        raise ValueError(f"{path}: truncated image ({img.size} of {meta['image_bytes']} bytes)")
+    if zlib.crc32(img) & 0xFFFFFFFF != meta["crc32"]:
+        raise ValueError(f"{path}: CRC mismatch")
+    t = torch.from_numpy(img)
+    return (t.to(device) if device is not None else t), meta
+
+
+def shard_parts(parts, tp_size, tp_rank):
+    """Rows of this rank from each part of a fused linear, stacked: [part0_p; part1_p; ...]."""
+    out = []
+    for w in parts:
+        lo, hi = shard_range(w.shape[0], tp_size, tp_rank)
+        out.append(w[lo:hi])
+    return torch.cat(out, 0).contiguous()
+
+
+def pack_fp16(w, device):
+    """fp16 [N, K] -> weight image on `device` (fq_quantize_pack_w6; needs the GPU)."""
+    from . import ops
+    wpk, _ = ops.quantize_pack_w6(w.to(device=device, dtype=torch.float16).contiguous())
+    return wpk
+
+
+LLAMA_LINEARS = [  # (file name, HF parts, activation bits)
+    ("attention.query_key_value", ("self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj"), 6),
+    ("attention.dense", ("self_attn.o_proj",), 6),
+    ("mlp.gate_up_proj", ("mlp.gate_proj", "mlp.up_proj"), 6),
+    ("mlp.down_proj", ("mlp.down_proj",), 8),
+]
+
+
+def convert_llama_safetensors(src, out_dir, tp_size=1, device="cuda:0", flex_down=True, layers=None):
+    """HF LLaMA safetensors (a file or a directory of *.safetensors) -> `.fqw6` files per linear
+    and rank + manifest.json.  Returns the manifest dict."""
+    from safetensors import safe_open  # no pickle: tensors only
+    files = [src] if os.path.isfile(src) else sorted(
+        os.path.join(src, f) for f in os.listdir(src) if f.endswith(".safetensors"))
+    where = {}
+    for fn in files:
+        with safe_open(fn, framework="pt") as f:
+            for k in f.keys():
+                where[k] = fn
+
+    def get(name):
+        with safe_open(where[name], framework="pt") as f:
+            return f.get_tensor(name)
+
+    n_layers = 1 + max(int(k.split(".")[2]) for k in where if k.startswith("model.layers."))
+    if layers is not None:
+        n_layers = min(n_layers, layers)
+    os.makedirs(out_dir, exist_ok=True)
+    manifest = dict(format="fqw6", version=VERSION, tp_size=tp_size, layers=n_layers, linears=[])
+    for li in range(n_layers):
+        for (fname, parts, ab) in LLAMA_LINEARS:
+            ws = [get(f"model.layers.{li}.{p}.weight").to(torch.float16) for p in parts]
+            K = ws[0].shape[1]
+            N_full = sum(w.shape[0] for w in ws)
+            abits = ab if flex_down else 6
+            for r in range(tp_size):
+                w_r = shard_parts(ws, tp_size, r)
+                img = pack_fp16(w_r, device)
+                path = os.path.join(out_dir, f"model.layers.{li}.{fname}.weight.{r}.fqw6")
+                save_image(path, img, w_r.shape[0], K, abits, N_full=N_full,
+                           row_offset=r * w_r.shape[0], tp_rank=r, tp_size=tp_size)
+                manifest["linears"].append(dict(layer=li, name=fname, rank=r, N=int(w_r.shape[0]), K=int(K),
+                                                N_full=int(N_full), abits=abits, parts=list(parts),
+                                                file=os.path.basename(path)))
+    with open(os.path.join(out_dir, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    return manifest
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="HF LLaMA safetensors -> flexq_amd packed W6 weight files")
+    ap.add_argument("src", help="a .safetensors file or a directory of them")
+    ap.add_argument("out", help="output directory")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks (column-parallel shards)")
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--no-flex-down", action="store_true", help="down_proj W6A6 instead of W6A8")
+    ap.add_argument("--layers", type=int, default=None)
+    a = ap.parse_args(argv)
+    m = convert_llama_safetensors(a.src, a.out, a.tp, a.device, not a.no_flex_down, a.layers)
+    print(f"wrote {len(m['linears'])} files for {m['layers']} layers, tp={a.tp} -> {a.out}")
+
+
+if __name__ == "__main__":
+    main()
