@@ -10,7 +10,7 @@ B="python3 bench.py --cpu-budget 0 --no-fp16-compare"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/kt -o run -- $B --steps 5 > gpurun_out/prof/kt.log 2>&1
 cp gpurun_out/prof/kt/run_kernel_stats.csv $P/${R}_kernel_stats.csv
 python3 tools/trace_summary.py gpurun_out/prof/kt/run_kernel_trace.csv > $P/${R}_kernel_trace_summary.txt
-tail -1 gpurun_out/prof/kt.log > $P/${R}_bench_under_rocprof.json
+grep '"metric"' gpurun_out/prof/kt.log | tail -1 > $P/${R}_bench_under_rocprof.json
 # 2. HBM traffic: FETCH_SIZE pass alone (no other counters), decode kernel only
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_decode -f csv -d gpurun_out/prof/pmc -o run -- $B --steps 2 --warmup 1 --roofline-reps 1 > gpurun_out/prof/pmc.log 2>&1
 cp gpurun_out/prof/pmc/run_counter_collection.csv $P/${R}_pmc_fetch_size.csv
