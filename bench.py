@@ -11,9 +11,12 @@ input, so by default they run as one linear over the concatenated weight image [
 (--no-merge: 5), one fq_linear_w6ax launch each (at decode sizes a single fused quantize+GEMM
 launch), the whole step captured into one HIP graph.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): column-parallel N-shard of every linear, each
-rank packs and streams only its N/P rows, then ONE all-gather per linear of the dequantized
-fp16 output over xGMI.  Total work is fixed, so "scaling" is "strong".
+Multi-GPU (torchrun, one process per GPU): by default (--parallel dp) every GPU is an independent
+replica serving its own token stream through the whole model (5 GB of packed weights per GPU);
+the data path has no collective, the ranks only meet at the timing barriers, and `value` sums
+the replicas ("scaling": "weak").  --parallel tp: column-parallel N-shard of every linear, each
+rank packs and streams only its N/P rows, then ONE RCCL all-gather per linear of the dequantized
+fp16 output over xGMI (the 70B N-shard case); total work is fixed ("strong").
 
 Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
 linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
@@ -268,6 +271,10 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
+    ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
+                    help="N > 1: dp = independent replicas, one token stream per GPU, no data-path collective "
+                         "(weak scaling); tp = every linear column-sharded over the N GPUs + one RCCL all-gather "
+                         "per linear (strong scaling, SURVEY.md §8(e))")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -283,12 +290,13 @@ def main():
     layers, M, lins, desc = cfg
     merge = not a.no_merge
     launch_lins = launch_list(lins, merge)
-    stack = build_stack(cfg, rank, world, dev, merge)
+    tp = world if a.parallel == "tp" else 1  # ranks one linear is sharded over
+    stack = build_stack(cfg, rank, tp, dev, merge)
     stream = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
 
     def step(gather=True):
-        run_step(stack, M, world, gather=gather)
+        run_step(stack, M, tp, gather=gather)
 
     # warm the per-stream workspace and RCCL communicators eagerly, on the capture stream
     with torch.cuda.stream(stream):
@@ -302,7 +310,7 @@ def main():
         try:
             graph = capture(step, stream)
         except RuntimeError as e:  # (an RCCL build that cannot be captured: time eager launches)
-            if world == 1:
+            if tp == 1:
                 raise
             print(f"[bench] rank {rank}: graph capture with RCCL failed ({e}); eager launches", file=sys.stderr)
             torch.cuda.synchronize()
@@ -341,13 +349,14 @@ def main():
     finite = bool(torch.isfinite(last.float()).all().item())
 
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
-    value = flops_step * a.steps / elapsed / 1e12
-    tok_s = M * a.steps / elapsed
+    replicas = world // tp  # independent token streams (dp), each through the whole model
+    value = replicas * flops_step * a.steps / elapsed / 1e12
+    tok_s = replicas * M * a.steps / elapsed
 
     # roofline of the dominant kernel (the decode linear): a graph of the step's linear launches
     # without the all-gathers, timed with HIP events on its stream
-    fused = {(N, K): ops.act_scratch_bytes(M, N // world, K) == 0 for (_, N, K, _) in launch_lins}
-    step_bytes = layers * sum(alg_bytes(M, N // world, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins)
+    fused = {(N, K): ops.act_scratch_bytes(M, N // tp, K) == 0 for (_, N, K, _) in launch_lins}
+    step_bytes = layers * sum(alg_bytes(M, N // tp, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins)
 
     def graph_time(fn, launches):
         g2 = capture(fn, stream)
@@ -359,15 +368,15 @@ def main():
         return t, t / (a.roofline_reps * launches)
 
     n_lin = layers * len(launch_lins)
-    if world == 1:  # the timed region itself: only the linear launches run in it
+    if tp == 1:  # the timed region itself: only the linear launches run in it (rank 0's)
         t_g = ev0.elapsed_time(ev1) / 1e3 * a.roofline_reps / a.steps
         per_launch_s = ev0.elapsed_time(ev1) / 1e3 / (a.steps * n_lin)
     else:  # without the all-gathers
         t_g, per_launch_s = graph_time(lambda: step(gather=False), n_lin)
     bytes_launch = step_bytes / n_lin
     achieved = bytes_launch / per_launch_s / 1e9
-    traffic, traffic_src = pmc_traffic(a.config, merge) if world == 1 else (None, None)
-    if world > 1:  # the same step without the all-gathers (max over ranks)
+    traffic, traffic_src = pmc_traffic(a.config, merge) if tp == 1 else (None, None)
+    if tp > 1:  # the same step without the all-gathers (max over ranks)
         tg = torch.tensor([t_g / a.roofline_reps], dtype=torch.float64, device=dev)
         dist.all_reduce(tg, op=dist.ReduceOp.MAX)
         gemm_only_ms = float(tg.item()) * 1e3
@@ -381,7 +390,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if tp > 1 else "weak",
         "vs_baseline": None,
         "dtype": "int8-mfma(w6a6)->fp16",
         "data": "synthetic (random-init int6 weights of the architecture with unit-gain scales; N(0,1) fp16 "
@@ -392,7 +401,8 @@ def main():
             "workload": desc + ", dependent linear stack of every decoder layer per step",
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
-            "parallelism": f"tp{world} column-parallel + RCCL all-gather per linear" if world > 1 else "single GPU",
+            "parallelism": (f"tp{world} column-parallel + RCCL all-gather per linear" if tp > 1 else
+                            f"dp{world}: independent replicas, one token stream per GPU, no data-path collective"),
             "graph": graph is not None,
             "launches_per_layer": [[name, N, K, ab] for (name, N, K, ab) in launch_lins],
         },
@@ -411,11 +421,11 @@ def main():
             "alg_bytes_per_launch": int(bytes_launch),
             "fused_launches": all(fused.values()),
             "method": ("HIP events on the launch stream around the timed steps (only the linear launches run)"
-                       if world == 1 else "graph of the step's linear launches only (no all-gather), HIP events "
+                       if tp == 1 else "graph of the step's linear launches only (no all-gather), HIP events "
                                           "on the capture stream"),
         },
     }
-    if world > 1:
+    if tp > 1:
         res["gemm_only_ms_per_step"] = round(gemm_only_ms, 4)
         res["allgather_bytes_per_step_per_rank"] = int(layers * sum(2 * M * (N // world) * (world - 1)
                                                                     for (_, N, K, _) in launch_lins))
