@@ -126,7 +126,6 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FQ_STAMP(0);
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
-    const int items = NT * S;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // All index math is 32-bit and divides at most once per launch (64-bit or per-item divisions
