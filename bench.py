@@ -51,7 +51,12 @@ CONFIGS = {
     "llama2-70b-m1": (80, 1, [("qkv", 10240, 8192, 6), ("o", 8192, 8192, 6), ("gate", 28672, 8192, 6),
                               ("up", 28672, 8192, 6), ("down", 8192, 28672, 6)],
                       "LLaMA-2-70B all linear shapes (GQA qkv), W6A6 g128, batch 1"),
+    # C5: prefill, seq 2048 x batch 8; every linear W6A8
+    "llama3-8b-prefill": (32, 16384, [("qkv", 6144, 4096, 8), ("o", 4096, 4096, 8), ("gate", 14336, 4096, 8),
+                                      ("up", 14336, 4096, 8), ("down", 4096, 14336, 8)],
+                          "LLaMA-3-8B all linear shapes, W6A8 g128, prefill seq 2048 x batch 8 (M = 16384)"),
 }
+PREFILL_M = 32  # above this the linear runs quantize + the MFMA-bound prefill GEMM (two launches)
 
 
 def alg_bytes(M, N, K, abits, fused=True):
@@ -88,8 +93,9 @@ def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
     layers, M, lins, _ = cfg
     g = torch.Generator(device=dev).manual_seed(seed + rank)
     stack = []
-    prev = torch.randn((M * lins[0][2],), dtype=torch.float16, device=dev, generator=g)  # the token
+    prev = torch.randn((M * lins[0][2],), dtype=torch.float16, device=dev, generator=g)  # the token(s)
     x_first = prev
+    shared = {}  # prefill: one output buffer per linear kind, reused by every layer (stream-ordered)
     for _ in range(layers):
         L = {}
         for (name, N, K, abits) in launch_list(lins, merge):
@@ -100,8 +106,15 @@ def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
             ws = ((torch.rand((K // GROUP, Nl), device=dev, generator=g) + 0.5) / (18.5 * 1.04 * K ** 0.5)).half()
             pk = ops.pack_w6(wq, ws)  # the weight image: 6-bit codes + blocked group scales
             del wq, ws
-            out = torch.empty((M, Nl), dtype=torch.float16, device=dev)
-            full = torch.empty((world * M * Nl,), dtype=torch.float16, device=dev) if world > 1 else None
+            if M > PREFILL_M:
+                if name not in shared:
+                    shared[name] = (torch.empty((M, Nl), dtype=torch.float16, device=dev),
+                                    torch.empty((world * M * Nl,), dtype=torch.float16, device=dev)
+                                    if world > 1 else None)
+                out, full = shared[name]
+            else:
+                out = torch.empty((M, Nl), dtype=torch.float16, device=dev)
+                full = torch.empty((world * M * Nl,), dtype=torch.float16, device=dev) if world > 1 else None
             src = prev if name != "up" else L["gate"]["x"].view(-1)
             x = src[:M * K].view(M, K)
             L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full, x=x)
@@ -227,35 +240,37 @@ def calibrate_peaks(dev, hbm_bytes=4 << 30, mfma_iters=20000):
                       "16x16x64 i8 MFMA chains per wave, 8 waves per CU"}
 
 
-def cpu_baseline(budget_s=15.0):
+def cpu_baseline(budget_s=15.0, lins=None, M=1):
     """The reference's CPU fake-quant QuantLinear forward (oracle restatement, torch CPU ops) on a
-    bounded sample: LLaMA-2-7B linear shapes at M=1, fp16, weights re-fake-quantised every forward
-    as the reference eval flow does (flexqllm.py:106-108 + int_linear.py:60-61)."""
+    bounded sample of the workload: its linear shapes, fp16, weights re-fake-quantised every
+    forward as the reference eval flow does (flexqllm.py:106-108 + int_linear.py:60-61); at
+    prefill sizes a 64-row slice of the M activation rows (the rate is per FLOP, so it scales)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fq_oracle as oracle  # bench's cpu_baseline leg only
     # the GPU box exports OMP_NUM_THREADS = its CPU share (os.cpu_count() reports the whole host)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    shapes = [(12288, 4096), (4096, 4096), (11008, 4096), (11008, 4096), (4096, 11008)]
+    lins = lins or CONFIGS["llama2-7b-m1"][2]
+    rows = min(M, 64)
     gen = torch.Generator().manual_seed(0)
-    ws = [torch.randn((N, K), generator=gen).mul_(0.02).half() for (N, K) in shapes]
-    xs = [torch.randn((1, K), generator=gen).half() for (N, K) in shapes]
+    ws = [torch.randn((N, K), generator=gen).mul_(0.02).half() for (_, N, K, _) in lins]
+    xs = [torch.randn((rows, K), generator=gen).half() for (_, N, K, _) in lins]
     flops = 0.0
     layers = 0
     t0 = time.perf_counter()
     while True:
-        for (N, K), w, x in zip(shapes, ws, xs):
-            oracle.quant_linear_forward(x, w, 6, 6, requant_weight=True)
-            flops += 2.0 * N * K
+        for (_, N, K, ab), w, x in zip(lins, ws, xs):
+            oracle.quant_linear_forward(x, w, 6, ab, requant_weight=True)
+            flops += 2.0 * rows * N * K
         layers += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     return dict(value=flops / dt / 1e12, unit="TFLOPS-equiv", cores=threads, kind="port",
-                sample=f"{layers} LLaMA-2-7B layers' 5 linears (M=1, fp16) through the fake-quant "
-                       f"QuantLinear forward with per-forward weight requantisation, {dt:.1f} s, "
-                       f"{1.0 * layers / dt / 32:.4f} tok/s-equivalent",
-                tok_per_s=layers / dt / 32)
+                sample=f"{layers} layers' {len(lins)} linears (M={rows} rows{' of ' + str(M) if rows < M else ''}, "
+                       f"fp16) through the fake-quant QuantLinear forward with per-forward weight "
+                       f"requantisation, {dt:.1f} s",
+                tok_per_s=rows * layers / dt / 32)
 
 
 def main():
@@ -368,6 +383,20 @@ def main():
         return t, t / (a.roofline_reps * launches)
 
     n_lin = layers * len(launch_lins)
+    prefill = M > PREFILL_M
+    if prefill:  # MFMA-bound: the dominant kernel is the prefill GEMM; time its launches alone
+        codes = {}
+        for name, p in linears(stack):
+            if name not in codes:
+                codes[name] = ops.quantize_act(p["x"], p["abits"])
+
+        def gemms():
+            for name, p in linears(stack):
+                ops.gemm_w6ax(codes[name][0], codes[name][1], p["pk"], p["Nl"], p["abits"], out=p["out"])
+
+        _, per_gemm_s = graph_time(gemms, n_lin)
+        ops_launch = layers * sum(2.0 * M * (N // tp) * K for (_, N, K, _) in launch_lins) / n_lin
+        del codes
     if tp == 1:  # the timed region itself: only the linear launches run in it (rank 0's)
         t_g = ev0.elapsed_time(ev1) / 1e3 * a.roofline_reps / a.steps
         per_launch_s = ev0.elapsed_time(ev1) / 1e3 / (a.steps * n_lin)
@@ -392,7 +421,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if tp > 1 else "weak",
         "vs_baseline": None,
-        "dtype": "int8-mfma(w6a6)->fp16",
+        "dtype": "int8-mfma(w6a%d)->fp16" % max(ab for (_, _, _, ab) in lins) if prefill else "int8-mfma(w6a6)->fp16",
         "data": "synthetic (random-init int6 weights of the architecture with unit-gain scales; N(0,1) fp16 "
                 "token, each linear reading the previous linear's output)",
         "outputs_finite": finite,
@@ -425,30 +454,54 @@ def main():
                                           "on the capture stream"),
         },
     }
+    if prefill:
+        ach = ops_launch / per_gemm_s / 1e12
+        res["roofline"] = {
+            "kernel": "fq_gemm_prefill_kernel",
+            "bound": "mfma",
+            "achieved": round(ach, 1),
+            "peak": I8_MFMA_PEAK_TOPS,
+            "unit": "TFLOP/s",
+            "frac": round(ach / I8_MFMA_PEAK_TOPS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "per_launch_us": round(per_gemm_s * 1e6, 3),
+            "alg_ops_per_launch": ops_launch,
+            "alg_bytes_per_launch": int(layers * sum(alg_bytes(M, N // tp, K, ab, False)
+                                                     for (_, N, K, ab) in launch_lins) / n_lin),
+            "step_ms_linears_incl_quantize": round(elapsed / a.steps * 1e3, 4),
+            "method": "graph of the step's prefill GEMM launches on pre-quantized codes (the quantize "
+                      "launches excluded), HIP events on the capture stream; TOPS = 2*M*N*K / launch time",
+        }
     if tp > 1:
         res["gemm_only_ms_per_step"] = round(gemm_only_ms, 4)
         res["allgather_bytes_per_step_per_rank"] = int(layers * sum(2 * M * (N // world) * (world - 1)
                                                                     for (_, N, K, _) in launch_lins))
     if world == 1 and not a.no_calibrate:
         res["roofline"]["peak_measured"] = calibrate_peaks(dev)
-        res["roofline"]["frac_of_measured"] = round(achieved / res["roofline"]["peak_measured"]["hbm_read_GBps"], 4)
+        pm = res["roofline"]["peak_measured"]
+        res["roofline"]["frac_of_measured"] = round(
+            (ach / pm["int8_mfma_TOPS"]) if prefill else (achieved / pm["hbm_read_GBps"]), 4)
     if world == 1 and not a.no_fp16_compare:
         del stack
         torch.cuda.empty_cache()
         shapes = sorted({(N, K) for (_, N, K, _) in lins})
-        cmp_cfg = fp16_compare(shapes, M, 6, dev)
-        cmp_ns = {m: fp16_compare(NORTH_STAR_SHAPES, m, 6, dev) for m in (1, 2, 4, 8)}
+        ab_cfg = max(ab for (_, _, _, ab) in lins)
+        cmp_cfg = fp16_compare(shapes, M, ab_cfg, dev, reps=20 if not prefill else 4)
         geo = lambda rows: round(float(np.exp(np.mean([np.log(r["speedup"]) for r in rows]))), 3)
         res["vs_rocblas_fp16"] = {
-            "what": "W6A6 linear (quantize+GEMM, one launch where fused) vs torch F.linear fp16 "
+            "what": f"W6A{ab_cfg} linear (quantize+GEMM, one launch where fused) vs torch F.linear fp16 "
                     "(hipBLASLt/rocBLAS), same M,N,K, graph-timed",
             "config_shapes": cmp_cfg, "config_geomean_speedup": geo(cmp_cfg),
-            "llama2_70b_m1": cmp_ns[1], "llama2_70b_m1_geomean_speedup": geo(cmp_ns[1]),
-            "llama2_70b_geomean_speedup_by_M": {str(m): geo(r) for m, r in cmp_ns.items()},
-            "north_star_target": 1.3,
         }
+        if not prefill:
+            cmp_ns = {m: fp16_compare(NORTH_STAR_SHAPES, m, 6, dev) for m in (1, 2, 4, 8)}
+            res["vs_rocblas_fp16"].update({
+                "llama2_70b_m1": cmp_ns[1], "llama2_70b_m1_geomean_speedup": geo(cmp_ns[1]),
+                "llama2_70b_geomean_speedup_by_M": {str(m): geo(r) for m, r in cmp_ns.items()},
+                "north_star_target": 1.3})
     if rank == 0 and world == 1 and a.cpu_budget > 0:
-        res["cpu_baseline"] = cpu_baseline(a.cpu_budget)
+        res["cpu_baseline"] = cpu_baseline(a.cpu_budget, lins, M)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
