@@ -13,15 +13,19 @@ File layout (little-endian, 64-byte header, then the image exactly as the GEMM r
   12 header bytes u32 (64)          40 abits    i32 (activation bits this linear runs with)
   16 N   i32 (rows in this file)    44 crc32    u32 of the image bytes
   20 K   i32                        48 image bytes u64 (= fq_packed_w_bytes(N, K))
-  24 N_full i32                     56 reserved (8 bytes, zero)
-  28 row_offset i32 (first row of this shard in the rank-major gathered output = rank * N)
+  24 N_full i32                     56 k_offset i32 (first weight column of a row-parallel shard)
+  28 row_offset i32 (first row of     60 split i32 (0 column-parallel: rows sharded; 1 row-parallel:
+     this shard in the rank-major        columns sharded on 128-group boundaries)
+     gathered output = rank * N)
 
-Tensor parallelism follows flexq_amd.dist: every linear is column-parallel (rank p owns output
-rows [p N/P, (p+1) N/P), 16-row aligned).  Fused linears shard their parts separately and stack
-them per rank (qkv = [q_p; k_p; v_p], gate_up = [gate_p; up_p], as FT's per-rank
-`3 * hidden / tp` layout), so a rank's gate and up halves meet in its own output for
-fq_silu_mul_quantize.  down_proj runs W6A8 (`--flex_linear_quant`, int_llama_layer.py:35-37),
-the others W6A6.
+Tensor parallelism is FT's decoder layout (`LlamaDecoderLayerWeight.cc:381-410`, flexq_amd.dist):
+qkv and gate_up are column-parallel, their parts sharded separately and stacked per rank
+(qkv = [q_p; k_p; v_p], gate_up = [gate_p; up_p], FT's per-rank `3 * hidden / tp` layout), so a
+rank's attention heads and its gate and up halves stay in its own output; attention.dense and
+down_proj are row-parallel (input columns [k_lo, k_hi), the rank's heads / its gate rows), summed
+by one all-reduce.  gate/up rows and down columns use the same 128-group split
+(dist.group_shard_range).  down_proj runs W6A8 (`--flex_linear_quant`,
+int_llama_layer.py:35-37), the others W6A6.
 
 Conversion runs the HIP packer (a GPU is required); reading and writing files does not.
 """
@@ -35,12 +39,12 @@ import numpy as np
 import torch
 
 from . import _lib
-from .dist import shard_range
+from .dist import group_shard_range, shard_range
 
 MAGIC = b"FQW6IMG\0"
 VERSION = 1
 HEADER = 64
-_FMT = "<8sIIiiiiiiiIQ8x"  # 64 bytes
+_FMT = "<8sIIiiiiiiiIQii"  # 64 bytes
 assert struct.calcsize(_FMT) == HEADER
 
 
@@ -48,7 +52,7 @@ def packed_bytes(N, K):
     return int(_lib.load().fq_packed_w_bytes(N, K))
 
 
-def save_image(path, image, N, K, abits, N_full=None, row_offset=0, tp_rank=0, tp_size=1):
+def save_image(path, image, N, K, abits, N_full=None, row_offset=0, tp_rank=0, tp_size=1, k_offset=0, split=0):
     """Write one weight image (uint8 tensor of fq_packed_w_bytes(N, K) bytes) with its header."""
     img = image.detach().to("cpu").contiguous().numpy().view(np.uint8).reshape(-1)
     if img.size != packed_bytes(N, K):
@@ -56,7 +60,7 @@ def save_image(path, image, N, K, abits, N_full=None, row_offset=0, tp_rank=0, t
     if abits not in (6, 8):
         raise ValueError("abits must be 6 or 8")
     hdr = struct.pack(_FMT, MAGIC, VERSION, HEADER, N, K, N if N_full is None else N_full, row_offset,
-                      tp_rank, tp_size, abits, zlib.crc32(img) & 0xFFFFFFFF, img.size)
+                      tp_rank, tp_size, abits, zlib.crc32(img) & 0xFFFFFFFF, img.size, k_offset, split)
     tmp = path + ".tmp"
     with open(tmp, "wb") as f:
         f.write(hdr)
@@ -69,11 +73,11 @@ def read_header(path):
         raw = f.read(HEADER)
     if len(raw) != HEADER:
         raise ValueError(f"{path}: truncated header")
-    magic, ver, hb, N, K, N_full, off, rank, size, abits, crc, nbytes = struct.unpack(_FMT, raw)
+    magic, ver, hb, N, K, N_full, off, rank, size, abits, crc, nbytes, k_off, split = struct.unpack(_FMT, raw)
     if magic != MAGIC or ver != VERSION or hb != HEADER:
         raise ValueError(f"{path}: not an fqw6 v{VERSION} file")
     return dict(N=N, K=K, N_full=N_full, row_offset=off, tp_rank=rank, tp_size=size, abits=abits, crc32=crc,
-                image_bytes=nbytes)
+                image_bytes=nbytes, k_offset=k_off, split=split)
 
 
 def load_image(path, device=None):
@@ -90,13 +94,21 @@ def load_image(path, device=None):
     return (t.to(device) if device is not None else t), meta
 
 
-def shard_parts(parts, tp_size, tp_rank):
-    """Rows of this rank from each part of a fused linear, stacked: [part0_p; part1_p; ...]."""
+def shard_parts(parts, tp_size, tp_rank, by_group=False):
+    """Rows of this rank from each part of a fused linear, stacked: [part0_p; part1_p; ...].
+    by_group: rows split on 128-group boundaries (gate/up, matching down_proj's column split)."""
     out = []
     for w in parts:
-        lo, hi = shard_range(w.shape[0], tp_size, tp_rank)
+        rng = group_shard_range if by_group else shard_range
+        lo, hi = rng(w.shape[0], tp_size, tp_rank)
         out.append(w[lo:hi])
     return torch.cat(out, 0).contiguous()
+
+
+def shard_columns(w, tp_size, tp_rank):
+    """Columns [k_lo, k_hi) of this rank (row-parallel), split on 128-group boundaries."""
+    lo, hi = group_shard_range(w.shape[1], tp_size, tp_rank)
+    return w[:, lo:hi].contiguous(), lo
 
 
 def pack_fp16(w, device):
@@ -106,11 +118,12 @@ def pack_fp16(w, device):
     return wpk
 
 
-LLAMA_LINEARS = [  # (file name, HF parts, activation bits)
-    ("attention.query_key_value", ("self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj"), 6),
-    ("attention.dense", ("self_attn.o_proj",), 6),
-    ("mlp.gate_up_proj", ("mlp.gate_proj", "mlp.up_proj"), 6),
-    ("mlp.down_proj", ("mlp.down_proj",), 8),
+COLUMN, ROW = 0, 1
+LLAMA_LINEARS = [  # (file name, HF parts, activation bits, split)
+    ("attention.query_key_value", ("self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj"), 6, COLUMN),
+    ("attention.dense", ("self_attn.o_proj",), 6, ROW),
+    ("mlp.gate_up_proj", ("mlp.gate_proj", "mlp.up_proj"), 6, COLUMN),
+    ("mlp.down_proj", ("mlp.down_proj",), 8, ROW),
 ]
 
 
@@ -136,19 +149,26 @@ def convert_llama_safetensors(src, out_dir, tp_size=1, device="cuda:0", flex_dow
     os.makedirs(out_dir, exist_ok=True)
     manifest = dict(format="fqw6", version=VERSION, tp_size=tp_size, layers=n_layers, linears=[])
     for li in range(n_layers):
-        for (fname, parts, ab) in LLAMA_LINEARS:
+        for (fname, parts, ab, split) in LLAMA_LINEARS:
             ws = [get(f"model.layers.{li}.{p}.weight").to(torch.float16) for p in parts]
             K = ws[0].shape[1]
             N_full = sum(w.shape[0] for w in ws)
             abits = ab if flex_down else 6
             for r in range(tp_size):
-                w_r = shard_parts(ws, tp_size, r)
+                k_off = row_off = 0
+                if split == ROW:
+                    w_r, k_off = shard_columns(ws[0], tp_size, r)
+                else:
+                    w_r = shard_parts(ws, tp_size, r, by_group=fname == "mlp.gate_up_proj")
+                    row_off = r * w_r.shape[0]
                 img = pack_fp16(w_r, device)
                 path = os.path.join(out_dir, f"model.layers.{li}.{fname}.weight.{r}.fqw6")
-                save_image(path, img, w_r.shape[0], K, abits, N_full=N_full,
-                           row_offset=r * w_r.shape[0], tp_rank=r, tp_size=tp_size)
-                manifest["linears"].append(dict(layer=li, name=fname, rank=r, N=int(w_r.shape[0]), K=int(K),
-                                                N_full=int(N_full), abits=abits, parts=list(parts),
+                save_image(path, img, w_r.shape[0], w_r.shape[1], abits, N_full=N_full, row_offset=row_off,
+                           tp_rank=r, tp_size=tp_size, k_offset=k_off, split=split)
+                manifest["linears"].append(dict(layer=li, name=fname, rank=r, N=int(w_r.shape[0]),
+                                                K=int(w_r.shape[1]), K_full=int(K), N_full=int(N_full),
+                                                abits=abits, parts=list(parts), k_offset=int(k_off),
+                                                split="row" if split == ROW else "column",
                                                 file=os.path.basename(path)))
     with open(os.path.join(out_dir, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)

@@ -11,26 +11,36 @@
     aq, as = silu_mul_quantize(gate, up, 8)                (activation_kernels.cu:245, A8)
     y      = W6A8 GEMM(aq, as)  (down_proj)                (FfnLayer.cc:540-558)
 
+`FlexQDecoderLayer` adds the attention half around a caller-supplied attention core (the core
+itself is out of scope): pre-attention RMSNorm + A6 codes -> qkv W6A6 -> attention
+-> o_proj W6A6 -> the FFN above -> residual (FT LlamaContextDecoder.cc:430-660 order).
+
 Every step runs the HIP kernels through the C ABI; nothing here computes on the CPU.  Weights come
-from `flexq_amd.convert` files or from fp16 tensors.  The block is one whole layer (TP 1); with
-the column-parallel shards of `flexq_amd.dist`, rank p's gate_up file holds [gate_p; up_p], so
-its SiLU step is rank-local, and down_proj (sharded by output rows, full K) needs the ranks' A8
-codes gathered first (one all-gather of M x F bytes + scales) before the per-rank down GEMM.
+from `flexq_amd.convert` files or from fp16 tensors.  Tensor parallelism is FT's layout
+(flexq_amd.dist): qkv and gate_up column-parallel (rank p's files hold [q_p; k_p; v_p] and
+[gate_p; up_p], so attention heads and SiLU*up are rank-local), o_proj and down_proj
+row-parallel over those rank-local inputs, each finished by ONE all-reduce of the fp16 partial
+outputs (RCCL over xGMI; `LlamaContextDecoder.cc:651`).  Two all-reduces per layer, no gathers.
 """
 import json
 import os
 
 import torch
+import torch.distributed as dist
 
 from . import convert, ops
+from .dist import all_reduce_sum
 
 
 class W6Linear:
     """One packed W6Ax linear: `image` (fq_packed_w_bytes(N, K) bytes on the device), N x K,
-    activations quantized to `abits` (6, or 8 for down_proj)."""
+    activations quantized to `abits` (6, or 8 for down_proj).  row_parallel: this is one rank's
+    column shard of a row-parallel linear; its outputs are partial sums, all-reduced over `group`
+    when called with reduce=True and the process group has more than one rank."""
 
-    def __init__(self, image, N, K, abits=6):
+    def __init__(self, image, N, K, abits=6, row_parallel=False, group=None):
         self.image, self.N, self.K, self.abits = image, N, K, abits
+        self.row_parallel, self.group = row_parallel, group
 
     @classmethod
     def from_fp16(cls, w, abits=6):
@@ -38,17 +48,23 @@ class W6Linear:
         return cls(img, w.shape[0], w.shape[1], abits)
 
     @classmethod
-    def from_file(cls, path, device):
+    def from_file(cls, path, device, group=None):
         img, meta = convert.load_image(path, device=device)
-        return cls(img, meta["N"], meta["K"], meta["abits"])
+        row = meta["split"] == convert.ROW and meta["tp_size"] > 1
+        return cls(img, meta["N"], meta["K"], meta["abits"], row_parallel=row, group=group)
 
-    def __call__(self, x, out=None):
+    def _finish(self, y, reduce):
+        if self.row_parallel and reduce and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            all_reduce_sum(y, self.group)
+        return y
+
+    def __call__(self, x, out=None, reduce=True):
         """fp16 [M, K] -> fp16 [M, N] (quantize + GEMM; one launch at decode sizes)."""
-        return ops.linear_w6ax(x, self.image, self.N, self.abits, out=out)
+        return self._finish(ops.linear_w6ax(x, self.image, self.N, self.abits, out=out), reduce)
 
-    def from_codes(self, xq, xs, out=None):
+    def from_codes(self, xq, xs, out=None, reduce=True):
         """Pre-quantized activations (a producer's output) -> fp16 [M, N]."""
-        return ops.gemm_w6ax(xq, xs, self.image, self.N, self.abits, out=out)
+        return self._finish(ops.gemm_w6ax(xq, xs, self.image, self.N, self.abits, out=out), reduce)
 
 
 class FlexQFfn:
@@ -63,21 +79,68 @@ class FlexQFfn:
         self.F = down.K
 
     @classmethod
-    def from_dir(cls, out_dir, layer, gamma, rank=0, device="cuda:0", eps=1e-6):
-        """Load one layer's FFN from flexq_amd.convert output (manifest.json + .fqw6 files)."""
-        m = json.load(open(os.path.join(out_dir, "manifest.json")))
-        files = {e["name"]: e["file"] for e in m["linears"] if e["layer"] == layer and e["rank"] == rank}
-        gu = W6Linear.from_file(os.path.join(out_dir, files["mlp.gate_up_proj"]), device)
-        dn = W6Linear.from_file(os.path.join(out_dir, files["mlp.down_proj"]), device)
+    def from_dir(cls, out_dir, layer, gamma, rank=0, device="cuda:0", eps=1e-6, group=None):
+        """Load one layer's FFN (rank `rank`'s shards) from flexq_amd.convert output."""
+        files = _layer_files(out_dir, layer, rank)
+        gu = W6Linear.from_file(os.path.join(out_dir, files["mlp.gate_up_proj"]), device, group)
+        dn = W6Linear.from_file(os.path.join(out_dir, files["mlp.down_proj"]), device, group)
         return cls(gu, dn, gamma.to(device=device, dtype=torch.float16), eps)
 
-    def __call__(self, residual, attn_out=None, return_intermediates=False):
+    def __call__(self, residual, attn_out=None, return_intermediates=False, reduce=True):
         """residual fp16 [M, H] (updated in place to residual + attn_out), attn_out fp16 [M, H] or
-        None -> FFN output fp16 [M, H] (the caller adds it to the residual)."""
+        None -> FFN output fp16 [M, H] (the caller adds it to the residual).  Tensor-parallel:
+        this rank's gate_up / down shards; reduce=False returns the rank's partial sum."""
         xq, xs = ops.rmsnorm_quantize(residual, self.gamma, self.gate_up.abits, eps=self.eps, input=attn_out)
         gu = self.gate_up.from_codes(xq, xs)
         aq, as_ = ops.silu_mul_quantize(gu[:, :self.F], gu[:, self.F:], self.down.abits)
-        y = self.down.from_codes(aq, as_)
+        y = self.down.from_codes(aq, as_, reduce=reduce)
         if return_intermediates:
             return y, dict(xq=xq, xs=xs, gate_up=gu, aq=aq, as_=as_)
         return y
+
+
+def _layer_files(out_dir, layer, rank):
+    m = json.load(open(os.path.join(out_dir, "manifest.json")))
+    return {e["name"]: e["file"] for e in m["linears"] if e["layer"] == layer and e["rank"] == rank}
+
+
+class FlexQDecoderLayer:
+    """One LLaMA decoder layer in FlexQ mode around a caller-supplied attention core
+    (FT `LlamaContextDecoder::forward`, int8_mode 5, LlamaContextDecoder.cc:430-660):
+
+        xq, xs = rmsnorm_quantize(h, gamma_attn, 6)               (pre-attention norm + A6 codes)
+        ctx    = attn_fn(qkv.from_codes(xq, xs))                  (rank-local heads: [M, 3H/P] -> [M, H/P])
+        a      = o_proj(ctx)           + all-reduce                (row-parallel, W6A6)
+        y      = FlexQFfn(h, a)        + all-reduce in down_proj   (h += a inside the fused norm)
+        h     += y
+
+    `attn_fn` is the out-of-scope attention (RoPE, KV cache, softmax): any callable mapping this
+    rank's qkv output [M, q + k + v columns] to its context [M, o_proj.K]."""
+
+    def __init__(self, qkv, o, ffn, gamma_attn, attn_fn, eps=1e-6):
+        if o.K % 128:
+            raise ValueError("o_proj input width must be whole 128-groups (head_dim 128 = one group)")
+        self.qkv, self.o, self.ffn, self.gamma_attn, self.attn_fn, self.eps = qkv, o, ffn, gamma_attn, attn_fn, eps
+
+    @classmethod
+    def from_dir(cls, out_dir, layer, gamma_attn, gamma_ffn, attn_fn, rank=0, device="cuda:0", eps=1e-6,
+                 group=None):
+        files = _layer_files(out_dir, layer, rank)
+        qkv = W6Linear.from_file(os.path.join(out_dir, files["attention.query_key_value"]), device, group)
+        o = W6Linear.from_file(os.path.join(out_dir, files["attention.dense"]), device, group)
+        ffn = FlexQFfn.from_dir(out_dir, layer, gamma_ffn, rank, device, eps, group)
+        return cls(qkv, o, ffn, gamma_attn.to(device=device, dtype=torch.float16), attn_fn, eps)
+
+    def attention(self, h, reduce=True):
+        """h fp16 [M, H] (not modified) -> attention output [M, H] (this rank's partial sum when
+        reduce=False)."""
+        xq, xs = ops.rmsnorm_quantize(h, self.gamma_attn, self.qkv.abits, eps=self.eps)
+        ctx = self.attn_fn(self.qkv.from_codes(xq, xs))
+        return self.o(ctx.contiguous(), reduce=reduce)
+
+    def __call__(self, h):
+        """h fp16 [M, H], updated in place to the layer output and returned."""
+        a = self.attention(h)
+        y = self.ffn(h, a)  # h += a (fused into the pre-FFN norm)
+        h += y
+        return h

@@ -18,7 +18,10 @@ def test_header_round_trip(tmp_path):
     back, meta = convert.load_image(p)
     assert torch.equal(back, img)
     assert meta == dict(N=N, K=K, N_full=96, row_offset=48, tp_rank=1, tp_size=2, abits=8,
-                        crc32=meta["crc32"], image_bytes=nb)
+                        crc32=meta["crc32"], image_bytes=nb, k_offset=0, split=convert.COLUMN)
+    convert.save_image(p, img, N, K, 6, N_full=N, tp_rank=1, tp_size=3, k_offset=384, split=convert.ROW)
+    meta = convert.read_header(p)
+    assert (meta["k_offset"], meta["split"], meta["row_offset"]) == (384, convert.ROW, 0)
     assert os.path.getsize(p) == convert.HEADER + nb
 
 
@@ -47,3 +50,17 @@ def test_fused_shards_stack_parts_per_rank():
     k = 100 + torch.arange(32).view(32, 1).expand(32, 2)
     r1 = convert.shard_parts([q, k], 2, 1)
     assert r1[:, 0].tolist() == list(range(32, 64)) + list(range(116, 132))
+
+
+def test_row_parallel_columns_and_matching_gate_rows():
+    """down_proj columns and gate/up rows use the same 128-group split, so rank p's SiLU*up
+    output is exactly down_proj's rank-local input."""
+    F, H, P = 640, 32, 2
+    down = torch.arange(H * F).view(H, F)
+    gate = torch.arange(F).view(F, 1).expand(F, 4)
+    for r in range(P):
+        cols, k_off = convert.shard_columns(down, P, r)
+        rows = convert.shard_parts([gate, gate], P, r, by_group=True)
+        assert rows.shape[0] == 2 * cols.shape[1]
+        assert rows[:cols.shape[1], 0].tolist() == list(range(k_off, k_off + cols.shape[1]))
+        assert torch.equal(cols, down[:, k_off:k_off + cols.shape[1]])

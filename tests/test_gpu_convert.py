@@ -1,7 +1,8 @@
 """GPU test of the offline converter (flexq_amd.convert): a tiny synthetic
 LLaMA checkpoint (safetensors, random fp16 weights -- no real checkpoint exists offline) is
 converted at TP 1 and 2; every file must hold exactly the image fq_quantize_pack_w6 makes of the
-rank's stacked shard, and a linear run from a loaded file must match the oracle."""
+rank's shard (stacked rows of qkv / gate_up, the 128-group column slice of o_proj / down_proj),
+and a linear run from a loaded file must match the oracle."""
 import json
 import os
 
@@ -42,8 +43,13 @@ def test_convert_llama(dev, ckpt, tmp_path, tp):
     assert json.load(open(tmp_path / "manifest.json"))["tp_size"] == tp
     for e in m["linears"]:
         parts = [t[f"model.layers.{e['layer']}.{p}.weight"] for p in e["parts"]]
-        w_r = convert.shard_parts(parts, tp, e["rank"])
         img, meta = convert.load_image(os.path.join(str(tmp_path), e["file"]), device=dev)
+        if e["split"] == "row":  # attention.dense, down_proj: the rank's 128-group column slice
+            w_r, k_off = convert.shard_columns(parts[0], tp, e["rank"])
+            assert meta["split"] == convert.ROW and meta["k_offset"] == k_off == e["k_offset"]
+        else:  # qkv, gate_up: the rank's rows of each part, stacked
+            w_r = convert.shard_parts(parts, tp, e["rank"], by_group=e["name"] == "mlp.gate_up_proj")
+            assert meta["split"] == convert.COLUMN
         assert (meta["N"], meta["K"], meta["tp_rank"], meta["abits"]) == (w_r.shape[0], w_r.shape[1], e["rank"],
                                                                           8 if "down" in e["name"] else 6)
         ref_img, ws = ops.quantize_pack_w6(w_r.to(dev))

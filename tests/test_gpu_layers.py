@@ -2,7 +2,9 @@
 -> SiLU*up -> A8 -> down W6A8, FT FfnLayer int8_mode 5).  Each stage is checked against the
 oracle on the block's own intermediate inputs (bit-exact where the stage is integer/bit-exact,
 oracle tolerance for the GEMMs), and the whole block against a float64 unquantized FFN
-(loose: W6A6/W6A8 quantization error), loaded from converter files at TP 1 and 2."""
+(loose: W6A6/W6A8 quantization error), loaded from converter files at TP 1 and 2 (FT's layout: column-parallel gate_up, row-parallel
+down_proj + all-reduce); the decoder layer (attention half around a stand-in attention core)
+likewise, and once through a real two-process all-reduce."""
 import numpy as np
 import pytest
 import torch
@@ -69,22 +71,33 @@ def test_ffn_stages_against_oracle(dev, weights, M):
     assert rel < 0.1, rel
 
 
-@pytest.mark.parametrize("tp", [1, 2])
-def test_ffn_from_converter_files(dev, weights, tmp_path, tp):
-    """Converter files: at TP 1 the FFN block loads and matches the block built from fp16 weights
-    bit for bit; at TP 2 each rank's gate_up image + SiLU*up is rank-local ([gate_p; up_p]) and the
-    ranks' A8 inputs of down_proj, concatenated, are the TP-1 ones."""
+def _ckpt(tmp_path, w, attn=None):
     from safetensors.torch import save_file
-    from flexq_amd import convert, ops
-    from flexq_amd.layers import FlexQFfn, W6Linear
-    w = weights
     t = {"model.layers.0.mlp.gate_proj.weight": w["gate"], "model.layers.0.mlp.up_proj.weight": w["up"],
          "model.layers.0.mlp.down_proj.weight": w["down"]}
     for n in ("q", "k", "v", "o"):  # (separate storage: safetensors refuses shared tensors)
-        t[f"model.layers.0.self_attn.{n}_proj.weight"] = w["down"][:, :H].clone()
+        t[f"model.layers.0.self_attn.{n}_proj.weight"] = (attn[n] if attn else w["down"][:, :H]).clone()
     save_file(t, str(tmp_path / "m.safetensors"))
+    return str(tmp_path / "m.safetensors")
+
+
+def ulp16(a):
+    return np.spacing(np.abs(a).astype(np.float16)).astype(np.float64)
+
+
+@pytest.mark.parametrize("tp", [1, 2])
+def test_ffn_from_converter_files(dev, weights, tmp_path, tp):
+    """Converter files (FT's TP layout): at TP 1 the FFN block loads and matches the block built
+    from fp16 weights bit for bit.  At TP 2 each rank runs its [gate_p; up_p] image, its SiLU*up
+    (rank-local A8 codes: concatenated, exactly the TP-1 codes, since the split is on 128-group
+    boundaries) and its row-parallel down_proj column slice (partial sum within the oracle
+    tolerance on its own codes); the partials' sum (what the all-reduce returns) is the TP-1
+    output within the full-K oracle tolerance plus one fp16 rounding per partial."""
+    from flexq_amd import convert
+    from flexq_amd.layers import FlexQFfn, W6Linear
+    w = weights
     out = str(tmp_path / "out")
-    m = convert.convert_llama_safetensors(str(tmp_path / "m.safetensors"), out, tp_size=tp, device=str(dev))
+    convert.convert_llama_safetensors(_ckpt(tmp_path, w), out, tp_size=tp, device=str(dev))
     x = torch.randn((4, H), generator=torch.Generator().manual_seed(9)).half().to(dev)
     ref = FlexQFfn(W6Linear.from_fp16(torch.cat([w["gate"], w["up"]]).to(dev), 6),
                    W6Linear.from_fp16(w["down"].to(dev), 8), w["gamma"].to(dev))
@@ -94,12 +107,141 @@ def test_ffn_from_converter_files(dev, weights, tmp_path, tp):
         y = ffn(x.clone())
         np.testing.assert_array_equal(host(y).view(np.uint16), host(y_ref).view(np.uint16))
         return
-    xq, xs = ops.rmsnorm_quantize(x.clone(), w["gamma"].to(dev), 6)
-    aqs = []
-    for e in m["linears"]:
-        if e["name"] != "mlp.gate_up_proj":
-            continue
-        gu = W6Linear.from_file(f"{out}/{e['file']}", dev).from_codes(xq, xs)
-        f = e["N"] // 2
-        aqs.append(ops.silu_mul_quantize(gu[:, :f], gu[:, f:], 8)[0])
-    np.testing.assert_array_equal(host(torch.cat(aqs, 1)), host(im_ref["aq"]))
+    aqs, parts = [], []
+    for r in range(tp):
+        ffn_r = FlexQFfn.from_dir(out, 0, w["gamma"], rank=r, device=dev)
+        assert ffn_r.down.row_parallel and not ffn_r.gate_up.row_parallel
+        y_r, im_r = ffn_r(x.clone(), None, return_intermediates=True, reduce=False)
+        cols, _ = convert.shard_columns(w["down"], tp, r)
+        wq, ws = oracle.quantize_engine(cols.numpy(), 6)
+        ref_r, _, mag_r = oracle.gemm(host(im_r["aq"]), host(im_r["as_"]), wq, ws)
+        assert_gemm_close(host(y_r), ref_r, mag_r, f"down_proj partial, rank {r}")
+        aqs.append(host(im_r["aq"]))
+        parts.append(host(y_r).astype(np.float64))
+    np.testing.assert_array_equal(np.concatenate(aqs, 1), host(im_ref["aq"]))
+    wq, ws = oracle.quantize_engine(w["down"].numpy(), 6)
+    ref_full, _, mag = oracle.gemm(host(im_ref["aq"]), host(im_ref["as_"]), wq, ws)
+    tol = oracle.gemm_tolerance(ref_full, mag) + sum(ulp16(p) for p in parts)
+    assert (np.abs(sum(parts) - ref_full.astype(np.float64)) <= tol).all()
+
+
+HD = 128  # head_dim = one quantization group
+
+
+def _attn_stand_in(qkv):
+    """Stand-in for the out-of-scope attention core: each head's context = its v slice (rank-local
+    per head, like the real core)."""
+    return qkv[:, 2 * qkv.shape[1] // 3:]
+
+
+def _decoder_weights():
+    g = torch.Generator().manual_seed(11)
+    return {n: (torch.randn((H, H), generator=g) / H ** 0.5).half() for n in ("q", "k", "v", "o")}
+
+
+@pytest.mark.parametrize("tp", [1, 2])
+def test_decoder_layer_tp(dev, weights, tmp_path, tp):
+    """FlexQDecoderLayer (FT LlamaContextDecoder order) from converter files.  TP 1: the attention
+    half against the oracle stage by stage, the layer against a float64 unquantized layer
+    (sanity bound).  TP 2, both ranks simulated on one GPU: each rank's o_proj partial on its own
+    heads and each rank's FFN partial, summed as the all-reduces would (fp16 sums), against TP 1."""
+    from flexq_amd import convert, ops
+    from flexq_amd.layers import FlexQDecoderLayer
+    w, aw = weights, _decoder_weights()
+    ga = (1 + 0.1 * torch.randn(H, generator=torch.Generator().manual_seed(12))).half()
+    out1, outp = str(tmp_path / "tp1"), str(tmp_path / "tpn")
+    ck = _ckpt(tmp_path, w, aw)
+    convert.convert_llama_safetensors(ck, out1, tp_size=1, device=str(dev))
+    x = torch.randn((5, H), generator=torch.Generator().manual_seed(13)).half()
+    L1 = FlexQDecoderLayer.from_dir(out1, 0, ga, w["gamma"], _attn_stand_in, device=dev)
+    a1 = L1.attention(x.to(dev))
+    h1 = L1(x.to(dev).clone())
+    # attention half against the oracle: A6 codes of the pre-attention norm, qkv, o_proj
+    _, _, q_ref, xs_ref = oracle.rmsnorm_quantize(None, x.numpy(), ga.numpy(), 1e-6, 6)
+    wq, ws = oracle.quantize_engine(torch.cat([aw["q"], aw["k"], aw["v"]]).numpy(), 6)
+    qkv_ref, _, mag = oracle.gemm(q_ref, xs_ref, wq, ws)
+    xq, xs = ops.rmsnorm_quantize(x.to(dev), ga.to(dev), 6)
+    qkv = L1.qkv.from_codes(xq, xs)
+    assert_gemm_close(host(qkv), qkv_ref, mag, "qkv")
+    cq, cs = oracle.quantize_engine(host(_attn_stand_in(qkv)), 6)
+    wq, ws = oracle.quantize_engine(aw["o"].numpy(), 6)
+    a_ref, _, mag_a = oracle.gemm(cq, cs, wq, ws)
+    assert_gemm_close(host(a1), a_ref, mag_a, "o_proj")
+    if tp == 1:
+        # the whole layer against float64 unquantized math (W6A6/W6A8 error only)
+        def rms(v, gm):
+            return v / np.sqrt((v * v).mean(1, keepdims=True) + 1e-6) * gm.numpy().astype(np.float64)
+        f = lambda t: t.numpy().astype(np.float64)  # noqa: E731
+        h = f(x)
+        n = rms(h, ga)
+        a = (n @ f(aw["v"]).T) @ f(aw["o"]).T
+        h = h + a
+        n = rms(h, w["gamma"])
+        gt, ut = n @ f(w["gate"]).T, n @ f(w["up"]).T
+        h = h + (gt / (1 + np.exp(-gt)) * ut) @ f(w["down"]).T
+        rel = np.linalg.norm(host(h1).astype(np.float64) - h) / np.linalg.norm(h)
+        assert rel < 0.05, rel
+        return
+    convert.convert_llama_safetensors(ck, outp, tp_size=tp, device=str(dev))
+    Ls = [FlexQDecoderLayer.from_dir(outp, 0, ga, w["gamma"], _attn_stand_in, rank=r, device=dev) for r in range(tp)]
+    assert all(L.o.row_parallel and L.o.K == H // tp for L in Ls)
+    a_parts = [L.attention(x.to(dev), reduce=False) for L in Ls]
+    a_sum = a_parts[0] + a_parts[1]  # the fp16 all-reduce of 2 ranks
+    tol = oracle.gemm_tolerance(a_ref, mag_a) + sum(ulp16(host(p)) for p in a_parts) + ulp16(a_ref)
+    assert (np.abs(host(a_sum).astype(np.float64) - a_ref.astype(np.float64)) <= tol).all()
+    # FFN half on the same input (h + the all-reduced attention output): a one-ulp difference in
+    # a_sum can flip a 6-bit code at a rounding boundary, so the TP-1 reference takes a_sum too
+    h = x.to(dev).clone()
+    y_parts = [L.ffn(h.clone(), a_sum, reduce=False) for L in Ls]
+    y1 = L1.ffn(h.clone(), a_sum)
+    y = host(y_parts[0] + y_parts[1]).astype(np.float64)
+    tol = 2e-3 * np.abs(host(y1).astype(np.float64)) + sum(ulp16(host(p)) for p in y_parts) + ulp16(host(y1))
+    assert (np.abs(y - host(y1).astype(np.float64)) <= tol).all()
+
+
+def _mp_worker(rank, world, port, out_dir, x, ga, gf, q):
+    import torch.distributed as dist
+    from flexq_amd.layers import FlexQDecoderLayer
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        L = FlexQDecoderLayer.from_dir(out_dir, 0, ga, gf, _attn_stand_in, rank=rank, device="cuda:0")
+        h = L(x.to("cuda:0").clone())
+        torch.cuda.synchronize()
+        q.put((rank, h.cpu()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_decoder_layer_two_processes(dev, weights, tmp_path):
+    """The real collective path: two ranks (processes) sharing the box's one GPU, the layer's two
+    all-reduces through torch.distributed (gloo here, RCCL on an 8-GPU node); both ranks end with
+    the same hidden state, equal to the one-GPU simulation of the same shards."""
+    import socket
+    import torch.multiprocessing as mp
+    from flexq_amd import convert
+    from flexq_amd.layers import FlexQDecoderLayer
+    w, aw = weights, _decoder_weights()
+    ga = (1 + 0.1 * torch.randn(H, generator=torch.Generator().manual_seed(12))).half()
+    out = str(tmp_path / "tp2")
+    convert.convert_llama_safetensors(_ckpt(tmp_path, w, aw), out, tp_size=2, device=str(dev))
+    x = torch.randn((3, H), generator=torch.Generator().manual_seed(14)).half()
+    Ls = [FlexQDecoderLayer.from_dir(out, 0, ga, w["gamma"], _attn_stand_in, rank=r, device=dev) for r in range(2)]
+    a = Ls[0].attention(x.to(dev), reduce=False) + Ls[1].attention(x.to(dev), reduce=False)
+    h = x.to(dev).clone()
+    y = Ls[0].ffn(h.clone(), a, reduce=False) + Ls[1].ffn(h.clone(), a, reduce=False)
+    h += a
+    h += y
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_mp_worker, args=(r, 2, port, out, x, ga, w["gamma"], q)) for r in range(2)]
+    for p_ in procs:
+        p_.start()
+    res = dict(q.get(timeout=100) for _ in range(2))
+    for p_ in procs:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    np.testing.assert_array_equal(res[0].numpy().view(np.uint16), res[1].numpy().view(np.uint16))
+    np.testing.assert_array_equal(res[0].numpy().view(np.uint16), host(h).view(np.uint16))
