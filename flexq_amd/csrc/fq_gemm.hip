@@ -485,13 +485,16 @@ __device__ __forceinline__ uint32_t ds_read_b32_at(uint32_t a) {
 // ABL (development ablations, FQ_DEV_ABLATION builds only): 1 = no dequant (accumulators kept
 // alive, no VALU), 2 = no MFMA (operands kept alive), 4 = no compute-side LDS reads, 8 = no
 // global loads / DMA, 16 = no output stores, 32 = no A DMA, 64 = no weight loads.
-template <bool DBG, int ABL = 0>
+// U8: the weights arrive already unpacked (fq_unpack_w8_kernel: the int8 B operands of every
+// (tile, group) exactly as unpack_w writes them to LDS, [NT][G][k-step][lane][16 B]), by LDS-DMA
+// with A into the same B stage: no plane buffer, no unpack VALU, no ds_write, one DMA stream.
+template <bool DBG, int ABL = 0, bool U8 = false>
 __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
-    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg) {
+    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu = nullptr) {
     __shared__ __attribute__((aligned(16))) char sa[2 * PF_ASTAGE];
     __shared__ __attribute__((aligned(16))) char sbu[2 * PF_BSTAGE];
-    __shared__ __attribute__((aligned(16))) char sraw[PF_WAVES * 3072];
+    __shared__ __attribute__((aligned(16))) char sraw[U8 ? 16 : PF_WAVES * 3072];
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
     const int lane = threadIdx.x & 63;
@@ -523,6 +526,12 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     const int btile = 2 * wid + (lane >> 5);  // tiles 2w, 2w + 1; block lanes 2j, 2j + 1
     const int bt = t0 + btile < NT ? t0 + btile : NT - 1;
     const char *bsrc = reinterpret_cast<const char *>(wpk) + (size_t)bt * G * FQ_BLOCK + (lane & 31) * 16;
+    const char *usrc[2];  // U8: tiles 2w, 2w + 1 of the unpacked operands, this lane's 16 B
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const int ut = t0 + 2 * wid + t < NT ? t0 + 2 * wid + t : NT - 1;
+        usrc[t] = wu + (size_t)ut * G * 2048 + lane * 16;
+    }
 
     const uint32_t la = lds_addr(sa), lbu = lds_addr(sbu);
     auto stage = [&](int g, int slot) {  // A + scales of group g -> A stage `slot` (PF_VM_A)
@@ -536,6 +545,14 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
             __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PF_XS_OFF + 64 * wid * 4), 2, 0, 0);
         else if (lane < (wid == 2 ? 16 : 1))
             __builtin_amdgcn_global_load_lds(wsrc + (wid == 2 ? g * 16 : 0), LDS_PTR(buf + (wid == 2 ? PF_WS_OFF : PF_PAD_OFF)), 16, 0, 0);
+        if (U8 && !(ABL & 64)) {
+            char *bdst = sbu + slot * PF_BSTAGE + 2 * wid * 2048;
+#pragma unroll
+            for (int t = 0; t < 2; t++)
+#pragma unroll
+                for (int k = 0; k < 2; k++)
+                    __builtin_amdgcn_global_load_lds(usrc[t] + (size_t)g * 2048 + k * 1024, LDS_PTR(bdst + t * 2048 + k * 1024), 16, 0, 0);
+        }
     };
     // The weight planes go through a small per-wave LDS buffer (DMA like A): values loaded into
     // VGPRs by inline asm a whole step before their use would be invisible to the register
@@ -588,12 +605,16 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
 
     // prologue: A stage 0 and the weights of group 0; unpack them; weights of group 1
     stage(0, 0);
-    load_w(0);
-    __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
-    read_w();
-    load_w(G > 1 ? 1 : 0);
-    unpack_w(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!U8) {
+        load_w(0);
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
+        read_w();
+        load_w(G > 1 ? 1 : 0);
+        unpack_w(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
+    }
 
     // Step g: barrier (A stage g, B operands g in LDS; every wave done with step g - 1) -> issue A
     // stage g + 1 -> the weights of group g + 1 (loaded a step ago) to registers, their buffer
@@ -603,10 +624,12 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         stage(g + 1 < G ? g + 1 : G - 1, (g + 1) & 1);  // past the last group: never-read copies,
-        __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_VM_A));  // so every path issues the same count
-        read_w();
-        load_w(g + 2 < G ? g + 2 : G - 1);
-        unpack_w((g + 1) & 1);
+        if (!U8) {                                       // so every path issues the same count
+            __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_VM_A));
+            read_w();
+            load_w(g + 2 < G ? g + 2 : G - 1);
+            unpack_w((g + 1) & 1);
+        }
 
         const uint32_t ab = la + (g & 1) * PF_ASTAGE, bb = lbu + (g & 1) * PF_BSTAGE + b_off;
         v4i b[4][2];
@@ -679,7 +702,7 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
         // A stage g + 1 landed (the weights of group g + 2 may stay in flight); the unpack writes
         // retired with the reads above.  (sched_barrier: keep the wait below the MFMA block.)
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_VM_W));
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(U8 ? 0 : PF_VM_W));
     }
     // the copies past the last group are still landing: LDS must be quiet before the WG retires
     __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
@@ -803,8 +826,32 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused) {
 
 static const size_t kTicketBytes = 256 * 1024;  // tickets for up to 65536 16-column tiles
 
+// Large-M prefill unpacks the weight image once per call into int8 B operands in the workspace
+// (0.75 B read + 1 B written per weight: ~1 % of the GEMM at M = 16384) so that the GEMM's B
+// path is a plain LDS-DMA stream (fq_gemm_prefill_kernel<U8>).
+constexpr int PF_U8_MIN_M = 2048;  // below, the unpack pass costs more than it saves (measured)
+static size_t prefill_u8_bytes(int N, int K) { return (size_t)((N + 15) / 16) * (K / FQ_GROUP) * 2048; }
+
+// One thread per (tile, group, block lane): its 8 bytes of each plane -> the two 16-byte int8
+// B operands (k-steps 0 and 1) that unpack_w writes for that lane.
+__global__ __launch_bounds__(256) void fq_unpack_w8_kernel(const char *__restrict__ img, long nblk,
+                                                          char *__restrict__ wu) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nblk * 64) return;
+    const long blk = i >> 6;
+    const int lane = (int)(i & 63);
+    const char *src = img + blk * FQ_BLOCK + lane * 8;
+    const uint2 p0 = *reinterpret_cast<const uint2 *>(src);
+    const uint2 p1 = *reinterpret_cast<const uint2 *>(src + 512);
+    const uint2 p2 = *reinterpret_cast<const uint2 *>(src + 1024);
+    char *dst = wu + blk * 2048 + lane * 16;
+    *reinterpret_cast<v4i *>(dst) = unpack_fq6(p0.x, p1.x, p2.x);
+    *reinterpret_cast<v4i *>(dst + 1024) = unpack_fq6(p0.y, p1.y, p2.y);
+}
+
 extern "C" size_t fq_gemm_workspace_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
+    if (M >= PF_U8_MIN_M) return prefill_u8_bytes(N, K);
     if (M > 32) return 0;
     const int S = decode_plan(M, N, K, false).S;  // the same for every staging variant and fused
     if (S == 1) return 0;
@@ -945,7 +992,7 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
 #define FQ_PABL(v)                                                                                         \
         if (abl == v)                                                                                        \
             hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, v>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs, \
-                               (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
+                               (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
         FQ_PABL(1) FQ_PABL(2) FQ_PABL(3) FQ_PABL(4) FQ_PABL(5) FQ_PABL(7) FQ_PABL(8) FQ_PABL(11) FQ_PABL(15)
         FQ_PABL(16) FQ_PABL(31) FQ_PABL(35) FQ_PABL(67) FQ_PABL(99)
 #undef FQ_PABL
@@ -953,12 +1000,28 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         return FQ_OK;
     }
 #endif
+    // Large M with room in the workspace: unpack once, then the U8 kernel (without a workspace the
+    // GEMM unpacks per WG; both are bit-identical)
+    if (M >= PF_U8_MIN_M && workspace && workspace_bytes >= prefill_u8_bytes(N, K)) {
+        const long nblk = (long)NT * (K / FQ_GROUP);
+        char *wu = (char *)workspace;
+        hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0, s,
+                           (const char *)w_packed, nblk, wu);
+        if (acc_dbg)
+            hipLaunchKernelGGL((fq_gemm_prefill_kernel<true, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
+        else
+            hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
+        FQ_LAUNCH_CHECK();
+        return FQ_OK;
+    }
     if (acc_dbg)
         hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs,
-                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
+                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
     else
         hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs,
-                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg);
+                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }

@@ -332,6 +332,34 @@ def test_bmma_state_api_reference_layout(ops, dev):
     assert_gemm_close(host(D), ref, mag, "bmma state api")
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (4096, 4096, 4096)])
+def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
+    """Large M with a workspace: the weights are unpacked once (fq_unpack_w8_kernel) and the GEMM
+    streams int8 operands (fq_gemm_prefill_kernel<U8>); without a workspace the GEMM unpacks per
+    workgroup.  Both paths: identical fp16 outputs and int32 accumulators."""
+    import ctypes
+    from flexq_amd import _lib
+    L = _lib.load()
+    assert L.fq_gemm_workspace_bytes(M, N, K) == ((N + 15) // 16) * (K // 128) * 2048
+    assert L.fq_gemm_workspace_bytes(M // 2 - 1, N, K) == 0
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    d1, a1 = ops.gemm_w6ax(xq, xs, pk, N, 8, return_acc=True)  # workspace: the unpacked path
+    d2 = torch.empty_like(d1)
+    a2 = torch.empty_like(a1)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = L.fq_gemm_w6ax(P(xq), P(xs), P(pk), M, N, K, 8, P(d2), P(a2), None, 0,
+                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert st == 0
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2)
+    assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
+
+
 @pytest.mark.parametrize("M,N,K,abits,with_acc", [
     (1000, 1000, 1280, 6, True),      # ragged M and N (partial WG tiles on both edges)
     (2048, 2048, 4096, 8, True),
