@@ -31,4 +31,13 @@ python3 tools/trace_summary.py gpurun_out/prof/m16/run_kernel_trace.csv > $P/${R
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/pf -o run -- python3 tools/prefill_bench.py 16384 > gpurun_out/prof/pf.log 2>&1
 python3 tools/trace_summary.py gpurun_out/prof/pf/run_kernel_trace.csv > $P/${R}_prefill_kernel_trace_summary.txt
 cp gpurun_out/prof/pf.log $P/${R}_prefill_bench.txt
+# 4. C5 (LLaMA-3-8B W6A8 prefill, M = 16384) bench under the kernel trace
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/c5 -o run -- $B --config llama3-8b-prefill --steps 2 --warmup 1 --no-calibrate > gpurun_out/prof/c5.log 2>&1
+python3 tools/trace_summary.py gpurun_out/prof/c5/run_kernel_trace.csv > $P/${R}_c5_kernel_trace_summary.txt
+grep '"metric"' gpurun_out/prof/c5.log | tail -1 > $P/${R}_c5_bench_under_rocprof.json
+# 5. prefill PMC passes (one GEMM shape) and their per-dispatch averages
+rm -rf gpurun_out/pf1 gpurun_out/pf2 gpurun_out/pf3 gpurun_out/pf4
+bash tools/pfprof.sh
+for i in 1 2 3 4; do python3 tools/pmc_avg.py gpurun_out/pf$i fq_gemm_prefill_kernel; done > $P/${R}_prefill_pmc.txt
+grep "TOPS" gpurun_out/pf1.log | tail -1 >> $P/${R}_prefill_pmc.txt
 echo profiles done
