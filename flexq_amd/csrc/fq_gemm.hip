@@ -851,7 +851,7 @@ __global__ __launch_bounds__(256) void fq_unpack_w8_kernel(const char *__restric
 
 extern "C" size_t fq_gemm_workspace_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
-    if (M >= PF_U8_MIN_M) return prefill_u8_bytes(N, K);
+    if (M >= PF_U8_MIN_M) return kTicketBytes + prefill_u8_bytes(N, K);  // tickets left untouched
     if (M > 32) return 0;
     const int S = decode_plan(M, N, K, false).S;  // the same for every staging variant and fused
     if (S == 1) return 0;
@@ -1002,9 +1002,11 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
 #endif
     // Large M with room in the workspace: unpack once, then the U8 kernel (without a workspace the
     // GEMM unpacks per WG; both are bit-identical)
-    if (M >= PF_U8_MIN_M && workspace && workspace_bytes >= prefill_u8_bytes(N, K)) {
+    if (M >= PF_U8_MIN_M && workspace && workspace_bytes >= kTicketBytes + prefill_u8_bytes(N, K)) {
         const long nblk = (long)NT * (K / FQ_GROUP);
-        char *wu = (char *)workspace;
+        // after the ticket region: one workspace serves both this and the split-K decode, whose
+        // tickets must stay zero between launches
+        char *wu = (char *)workspace + kTicketBytes;
         hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0, s,
                            (const char *)w_packed, nblk, wu);
         if (acc_dbg)

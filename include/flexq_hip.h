@@ -62,7 +62,11 @@ const char *fq_status_string(fq_status s);
  * 16 columns x 128 k (1536 B codes + 32 B scales). */
 size_t fq_packed_w_bytes(int N, int K);
 /* Bytes of scratch fq_gemm_w6ax / fq_linear_w6ax need for this shape (0 if none).  The buffer
- * must be zero-filled once after allocation (fq_workspace_init); the kernels leave it zeroed. */
+ * must be zero-filled once after allocation (fq_workspace_init).  Layout: a 256 KiB ticket
+ * region (split-K decode, M <= 32; the kernels leave it zeroed) followed by the split-K slabs
+ * or, for M >= 2048, the unpacked int8 weights of the prefill GEMM (rewritten every call).  One
+ * buffer of the largest size may serve every shape on one stream.  Prefill without a workspace
+ * (or a smaller one) still runs, with the weights unpacked per workgroup (bit-identical). */
 size_t fq_gemm_workspace_bytes(int M, int N, int K);
 fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_t stream);
 

@@ -332,6 +332,34 @@ def test_bmma_state_api_reference_layout(ops, dev):
     assert_gemm_close(host(D), ref, mag, "bmma state api")
 
 
+def test_split_k_after_prefill_on_shared_workspace(ops, dev):
+    """One workspace per stream serves the large-M unpack buffer and the split-K decode tickets:
+    a split-K decode launch right after a prefill launch on the same stream is still exact."""
+    from flexq_amd import _lib
+    L = _lib.load()
+    Md, Nd, Kd = 1, 512, 8192  # split-K shape (workspace > 0 at M = 1)
+    assert L.fq_gemm_workspace_bytes(Md, Nd, Kd) > 0
+    g = torch.Generator(device=dev).manual_seed(3)
+    xq = torch.randint(-32, 32, (Md, Kd), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((Kd // 128, Md), device=dev, generator=g) * 0.05).half()
+    wq = torch.randint(-32, 32, (Nd, Kd), dtype=torch.int8, device=dev, generator=g)
+    ws = (torch.rand((Kd // 128, Nd), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    d0 = ops.gemm_w6ax(xq, xs, pk, Nd, 6)
+    Mp, Np, Kp = 2048, 2048, 4096  # prefill on the same stream: the unpack buffer is written
+    xp = torch.randint(-128, 128, (Mp, Kp), dtype=torch.int8, device=dev, generator=g)
+    xsp = (torch.rand((Kp // 128, Mp), device=dev, generator=g) * 0.05).half()
+    pkp = ops.pack_w6(torch.randint(-32, 32, (Np, Kp), dtype=torch.int8, device=dev, generator=g),
+                      (torch.rand((Kp // 128, Np), device=dev, generator=g) * 0.05).half())
+    ops.gemm_w6ax(xp, xsp, pkp, Np, 8)
+    for _ in range(3):
+        d1 = ops.gemm_w6ax(xq, xs, pk, Nd, 6)
+        torch.cuda.synchronize()
+        assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+    ref, _, mag = oracle.gemm(host(xq), host(xs), host(wq), host(ws))
+    assert_gemm_close(host(d1), ref, mag, "split-K after prefill")
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (4096, 4096, 4096)])
 def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     """Large M with a workspace: the weights are unpacked once (fq_unpack_w8_kernel) and the GEMM
@@ -340,7 +368,7 @@ def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     import ctypes
     from flexq_amd import _lib
     L = _lib.load()
-    assert L.fq_gemm_workspace_bytes(M, N, K) == ((N + 15) // 16) * (K // 128) * 2048
+    assert L.fq_gemm_workspace_bytes(M, N, K) == 256 * 1024 + ((N + 15) // 16) * (K // 128) * 2048
     assert L.fq_gemm_workspace_bytes(M // 2 - 1, N, K) == 0
     g = torch.Generator(device=dev).manual_seed(M + N)
     xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
