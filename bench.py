@@ -11,12 +11,15 @@ input, so by default they run as one linear over the concatenated weight image [
 (--no-merge: 5), one fq_linear_w6ax launch each (at decode sizes a single fused quantize+GEMM
 launch), the whole step captured into one HIP graph.
 
-Multi-GPU (torchrun, one process per GPU): by default (--parallel dp) every GPU is an independent
-replica serving its own token stream through the whole model (5 GB of packed weights per GPU);
-the data path has no collective, the ranks only meet at the timing barriers, and `value` sums
-the replicas ("scaling": "weak").  --parallel tp: column-parallel N-shard of every linear, each
-rank packs and streams only its N/P rows, then ONE RCCL all-gather per linear of the dequantized
-fp16 output over xGMI (the 70B N-shard case); total work is fixed ("strong").
+Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself through a child torchrun
+when it is not already under one): by default every linear is column-parallel over the N GPUs
+(BASELINE config C4's scheme): each rank packs and streams only its N/P rows,
+then ONE RCCL all-gather per linear assembles the dequantized fp16 output over xGMI; total work
+is fixed ("scaling": "strong"), `value` is the whole model's TFLOPS-equiv per step time (max
+over ranks).  The same line reports the step without the gathers (GEMM only), the per-rank HBM
+fraction, the gather bytes, the same model as independent replicas (`replicas`, --parallel dp:
+no data-path collective, weak scaling) and the LLaMA-2-70B column-parallel stack
+(`c4_llama2_70b_tp`).
 
 Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
 linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
@@ -129,14 +132,19 @@ def linears(stack):
     return [(n, p) for L in stack for n, p in L.items() if not n.startswith("_")]
 
 
-def run_step(stack, M, world, group=None, gather=True):
+def run_step(stack, M, world, group=None, gather=True, staged=False):
     """One token through the linear stack, one launch per linear: fq_linear_w6ax (decode sizes:
     one fused quantize+GEMM launch each), then one RCCL all-gather of the fp16 shard outputs per
-    linear when world > 1."""
+    linear when world > 1 (staged: through host memory, for the gloo rehearsal of --share-gpu)."""
     for name, p in linears(stack):
         ops.linear_w6ax(p["x"], p["pk"], p["Nl"], p["abits"], out=p["out"])
         if world > 1 and gather:
-            dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
+            if staged:
+                full = torch.empty(p["full"].shape, dtype=p["full"].dtype)
+                dist.all_gather_into_tensor(full, p["out"].view(-1).cpu(), group=group)
+                p["full"].copy_(full)
+            else:
+                dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
 
 
 def capture(fn, stream):
@@ -240,11 +248,26 @@ def calibrate_peaks(dev, hbm_bytes=4 << 30, mfma_iters=20000):
                       "16x16x64 i8 MFMA chains per wave, 8 waves per CU"}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(budget_s=15.0, lins=None, M=1):
     """The reference's CPU fake-quant QuantLinear forward (oracle restatement, torch CPU ops) on a
-    bounded sample of the workload: its linear shapes, fp16, weights re-fake-quantised every
-    forward as the reference eval flow does (flexqllm.py:106-108 + int_linear.py:60-61); at
-    prefill sizes a 64-row slice of the M activation rows (the rate is per FLOP, so it scales)."""
+    bounded sample of the workload's linear shapes, fp16, in BASELINE.md §3's two variants, half
+    the budget each:
+      * pre-quantized weights (weight_quant_inplace once, flexq_quantize/utils.py:116-123, then
+        only the dynamic activation quantizer + F.linear per forward) -- the primary `value`;
+      * re-quantized weights per forward: the reference eval flow (flexqllm.py:106-108 leaves
+        use_weight_quant on, int_linear.py:60-61).
+    At prefill sizes a 64-row slice of the M activation rows (the rate is per FLOP, so it scales)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fq_oracle as oracle  # bench's cpu_baseline leg only
     # the GPU box exports OMP_NUM_THREADS = its CPU share (os.cpu_count() reports the whole host)
@@ -255,27 +278,169 @@ def cpu_baseline(budget_s=15.0, lins=None, M=1):
     gen = torch.Generator().manual_seed(0)
     ws = [torch.randn((N, K), generator=gen).mul_(0.02).half() for (_, N, K, _) in lins]
     xs = [torch.randn((rows, K), generator=gen).half() for (_, N, K, _) in lins]
-    flops = 0.0
-    layers = 0
-    t0 = time.perf_counter()
-    while True:
-        for (_, N, K, ab), w, x in zip(lins, ws, xs):
-            oracle.quant_linear_forward(x, w, 6, ab, requant_weight=True)
-            flops += 2.0 * rows * N * K
-        layers += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return dict(value=flops / dt / 1e12, unit="TFLOPS-equiv", cores=threads, kind="port",
-                sample=f"{layers} layers' {len(lins)} linears (M={rows} rows{' of ' + str(M) if rows < M else ''}, "
-                       f"fp16) through the fake-quant QuantLinear forward with per-forward weight "
-                       f"requantisation, {dt:.1f} s",
-                tok_per_s=rows * layers / dt / 32)
+    what = [oracle.fake_quant_per_group(w, 6)[0] for w in ws]  # weight_quant_inplace, once
+
+    def run(requant, budget):
+        flops, layers = 0.0, 0
+        t0 = time.perf_counter()
+        while True:
+            for (_, N, K, ab), w, wh, x in zip(lins, ws, what, xs):
+                oracle.quant_linear_forward(x, w, 6, ab, requant_weight=requant, w_hat=wh)
+                flops += 2.0 * rows * N * K
+            layers += 1
+            if time.perf_counter() - t0 > budget:
+                break
+        dt = time.perf_counter() - t0
+        return flops / dt / 1e12, layers, dt
+
+    pre, pre_layers, pre_dt = run(False, budget_s / 2)
+    req, req_layers, req_dt = run(True, budget_s / 2)
+    sample = (f"{len(lins)} linears per layer at M={rows} rows{' of ' + str(M) if rows < M else ''}, fp16, "
+              f"through the fake-quant QuantLinear forward")
+    return dict(value=pre, unit="TFLOPS-equiv", cores=threads, kind="port",
+                sample=f"{sample}: {pre_layers} layers in {pre_dt:.1f} s with pre-quantized weights",
+                tok_per_s=rows * pre_layers / pre_dt / 32,
+                cpu_model=cpu_model(), os_cpu_count=os.cpu_count(), torch_threads=torch.get_num_threads(),
+                variants={
+                    "prequantized_weights": dict(value=pre, tok_per_s=rows * pre_layers / pre_dt / 32,
+                                                 layers=pre_layers, seconds=round(pre_dt, 2)),
+                    "requant_weights_per_forward": dict(value=req, tok_per_s=rows * req_layers / req_dt / 32,
+                                                        layers=req_layers, seconds=round(req_dt, 2),
+                                                        note="the reference eval flow (flexqllm.py:106-108)"),
+                })
+
+
+def spawn_ranks(a):
+    """`bench.py --gpus N` outside torchrun: start N ranks as a child torchrun (one process per GPU,
+    127.0.0.1 rendezvous) and return its exit code.  Runs before anything touches the GPU
+    (torch.cuda.device_count() does not initialise it on this image), and the child is a separate
+    process: nothing is exec'd over a process that has used the GPU."""
+    import socket
+    import subprocess
+    n_dev = torch.cuda.device_count()
+    if n_dev < a.gpus and not a.share_gpu:
+        print(f"[bench] --gpus {a.gpus} but only {n_dev} GPU(s) visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class Ctx:
+    """Rank context: device, world, the timing helpers shared by every measured stack."""
+
+    def __init__(self, a, rank, world, dev, staged):
+        self.a, self.rank, self.world, self.dev, self.staged = a, rank, world, dev, staged
+        self.stream = torch.cuda.Stream(dev)
+
+    def sync_all(self):
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(self, v):
+        if self.world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def prepare(self, step, use_graph):
+        """Warm `step` eagerly on the capture stream (workspaces, communicators), then capture it
+        into one HIP graph when allowed; returns replay()."""
+        with torch.cuda.stream(self.stream):
+            step()
+        self.sync_all()
+        graph = None
+        if use_graph:
+            try:
+                graph = capture(step, self.stream)
+            except RuntimeError as e:  # (an RCCL build that cannot be captured: time eager launches)
+                if self.world == 1:
+                    raise
+                print(f"[bench] rank {self.rank}: graph capture with RCCL failed ({e}); eager launches",
+                      file=sys.stderr)
+                torch.cuda.synchronize()
+        if graph is None:
+            def replay():
+                with torch.cuda.stream(self.stream):
+                    step()
+        else:
+            def replay():
+                graph.replay()
+        replay.graph = graph
+        return replay
+
+    def timed(self, replay, steps, warmup):
+        """W untimed + K timed replays, barrier + synchronize on both sides; the max over ranks of
+        the wall time, and this rank's HIP-event time on the launch stream."""
+        with torch.cuda.stream(self.stream):
+            for _ in range(warmup):
+                replay()
+        self.sync_all()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(self.stream):
+            ev0.record(self.stream)
+            for _ in range(steps):
+                replay()
+            ev1.record(self.stream)
+        self.sync_all()
+        elapsed = time.perf_counter() - t0
+        return self.max_over_ranks(elapsed), ev0.elapsed_time(ev1) / 1e3
+
+    def graph_time(self, fn, launches, reps):
+        """Seconds per replay and per launch of a graph of fn (HIP events on its stream)."""
+        g2 = capture(fn, self.stream)
+        for _ in range(2):
+            g2.replay()
+        torch.cuda.synchronize()
+        t = time_graph(g2, reps, self.stream)
+        del g2
+        return t / reps, t / (reps * launches)
+
+
+def measure_tp(ctx, cfg, merge, tp, steps, warmup):
+    """Column-parallel N-shard of every linear of cfg over tp ranks: each rank
+    streams its N/tp rows, ONE all-gather per linear assembles the fp16 output.  Returns ms/step
+    with and without the gathers (max over ranks), the per-rank roofline of the GEMM launches and
+    the gather bytes."""
+    layers, M, lins, _ = cfg
+    launch_lins = launch_list(lins, merge)
+    stack = build_stack(cfg, ctx.rank, tp, ctx.dev, merge)
+    use_graph = not ctx.a.no_graph and not ctx.staged
+    replay = ctx.prepare(lambda: run_step(stack, M, tp, staged=ctx.staged), use_graph)
+    elapsed, _ = ctx.timed(replay, steps, warmup)
+    n_lin = layers * len(launch_lins)
+    gemm_step, per_launch = ctx.graph_time(lambda: run_step(stack, M, tp, gather=False), n_lin,
+                                           ctx.a.roofline_reps)
+    finite = bool(torch.isfinite(linears(stack)[-1][1]["full"].float()).all().item())
+    gemm_ms = ctx.max_over_ranks(gemm_step) * 1e3
+    per_launch = ctx.max_over_ranks(per_launch)
+    fused = {(N, K): ops.act_scratch_bytes(M, N // tp, K) == 0 for (_, N, K, _) in launch_lins}
+    bytes_launch = layers * sum(alg_bytes(M, N // tp, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins) / n_lin
+    flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)
+    del stack, replay
+    torch.cuda.empty_cache()
+    return dict(ms_per_step=elapsed / steps * 1e3, elapsed=elapsed, flops_step=flops_step,
+                gemm_only_ms_per_step=gemm_ms, allgather_ms_per_step=max(0.0, elapsed / steps * 1e3 - gemm_ms),
+                per_launch_us=per_launch * 1e6, alg_bytes_per_launch=int(bytes_launch),
+                hbm_GBps_per_rank=bytes_launch / per_launch / 1e9,
+                allgather_bytes_per_step_per_rank=int(layers * sum(2 * M * (N // tp) * (tp - 1)
+                                                                   for (_, N, K, _) in launch_lins)),
+                launches_per_step=n_lin, fused_launches=all(fused.values()), graph=use_graph, finite=finite)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); outside torchrun, N > 1 starts them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="llama2-7b-m1", choices=sorted(CONFIGS))
@@ -286,130 +451,90 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
-    ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
-                    help="N > 1: dp = independent replicas, one token stream per GPU, no data-path collective "
-                         "(weak scaling); tp = every linear column-sharded over the N GPUs + one RCCL all-gather "
-                         "per linear (strong scaling, SURVEY.md §8(e))")
+    ap.add_argument("--parallel", choices=["dp", "tp"], default=None,
+                    help="N > 1: tp (default) = every linear column-sharded over the N GPUs + one RCCL "
+                         "all-gather per linear, total work fixed (strong scaling, SURVEY.md §8(e)); "
+                         "dp = independent replicas, one token stream per GPU (weak scaling)")
+    ap.add_argument("--no-replicas", action="store_true", help="N > 1, tp: skip the replica (dp) measurement")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N > 1: skip the LLaMA-2-70B column-parallel measurement (BASELINE config C4)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:0, gloo with host-staged gathers, no graph")
     a = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if world != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world}: launch N ranks with torchrun "
+              f"--nproc-per-node N, or run bench.py --gpus N without torchrun", file=sys.stderr)
+        sys.exit(2)
+    staged = a.share_gpu and world > 1
+    dev = torch.device("cuda", 0 if a.share_gpu else local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if staged:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    ctx = Ctx(a, rank, world, dev, staged)
 
     cfg = CONFIGS[a.config]
     layers, M, lins, desc = cfg
     merge = not a.no_merge
     launch_lins = launch_list(lins, merge)
-    tp = world if a.parallel == "tp" else 1  # ranks one linear is sharded over
-    stack = build_stack(cfg, rank, tp, dev, merge)
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.synchronize()
-
-    def step(gather=True):
-        run_step(stack, M, tp, gather=gather)
-
-    # warm the per-stream workspace and RCCL communicators eagerly, on the capture stream
-    with torch.cuda.stream(stream):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-
-    graph = None
-    if not a.no_graph:
-        try:
-            graph = capture(step, stream)
-        except RuntimeError as e:  # (an RCCL build that cannot be captured: time eager launches)
-            if tp == 1:
-                raise
-            print(f"[bench] rank {rank}: graph capture with RCCL failed ({e}); eager launches", file=sys.stderr)
-            torch.cuda.synchronize()
-    if graph is None:
-        def replay():
-            with torch.cuda.stream(stream):
-                step()
-    else:
-        def replay():
-            graph.replay()
-
-    with torch.cuda.stream(stream):
-        for _ in range(a.warmup):
-            replay()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        ev0.record(stream)  # HIP events on the launch stream, bracketing exactly the timed steps
-        for _ in range(a.steps):
-            replay()
-        ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    last = linears(stack)[-1][1]["out"]
-    finite = bool(torch.isfinite(last.float()).all().item())
-
-    flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
-    replicas = world // tp  # independent token streams (dp), each through the whole model
-    value = replicas * flops_step * a.steps / elapsed / 1e12
-    tok_s = replicas * M * a.steps / elapsed
-
-    # roofline of the dominant kernel (the decode linear): a graph of the step's linear launches
-    # without the all-gathers, timed with HIP events on its stream
-    fused = {(N, K): ops.act_scratch_bytes(M, N // tp, K) == 0 for (_, N, K, _) in launch_lins}
-    step_bytes = layers * sum(alg_bytes(M, N // tp, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins)
-
-    def graph_time(fn, launches):
-        g2 = capture(fn, stream)
-        for _ in range(2):
-            g2.replay()
-        torch.cuda.synchronize()
-        t = time_graph(g2, a.roofline_reps, stream)
-        del g2
-        return t, t / (a.roofline_reps * launches)
-
-    n_lin = layers * len(launch_lins)
+    parallel = a.parallel or ("tp" if world > 1 else "dp")
+    tp = world if parallel == "tp" else 1  # ranks one linear is sharded over
     prefill = M > PREFILL_M
-    if prefill:  # MFMA-bound: the dominant kernel is the prefill GEMM; time its launches alone
-        codes = {}
-        for name, p in linears(stack):
-            if name not in codes:
-                codes[name] = ops.quantize_act(p["x"], p["abits"])
+    n_lin = layers * len(launch_lins)
+    flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
 
-        def gemms():
+    if tp > 1:
+        r = measure_tp(ctx, cfg, merge, tp, a.steps, a.warmup)
+        elapsed = r["elapsed"]
+        value = flops_step * a.steps / elapsed / 1e12
+        tok_s = M * a.steps / elapsed
+        per_launch_s = r["per_launch_us"] / 1e6
+        bytes_launch = r["alg_bytes_per_launch"]
+        fused_all = r["fused_launches"]
+        use_graph = r["graph"]
+        finite = r["finite"]
+    else:
+        stack = build_stack(cfg, rank, 1, dev, merge)
+        use_graph = not a.no_graph
+        replay = ctx.prepare(lambda: run_step(stack, M, 1), use_graph)
+        elapsed, ev_s = ctx.timed(replay, a.steps, a.warmup)
+        replicas = world  # independent token streams (dp), each through the whole model
+        value = replicas * flops_step * a.steps / elapsed / 1e12
+        tok_s = replicas * M * a.steps / elapsed
+        # roofline of the dominant kernel: the timed region itself (only the linear launches run
+        # in it), HIP events on the launch stream
+        per_launch_s = ev_s / (a.steps * n_lin)
+        fused = {(N, K): ops.act_scratch_bytes(M, N, K) == 0 for (_, N, K, _) in launch_lins}
+        fused_all = all(fused.values())
+        bytes_launch = layers * sum(alg_bytes(M, N, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins) / n_lin
+        last = linears(stack)[-1][1]["out"]
+        finite = bool(torch.isfinite(last.float()).all().item())
+        if prefill:  # MFMA-bound: the dominant kernel is the prefill GEMM; time its launches alone
+            codes = {}
             for name, p in linears(stack):
-                ops.gemm_w6ax(codes[name][0], codes[name][1], p["pk"], p["Nl"], p["abits"], out=p["out"])
+                if name not in codes:
+                    codes[name] = ops.quantize_act(p["x"], p["abits"])
 
-        _, per_gemm_s = graph_time(gemms, n_lin)
-        ops_launch = layers * sum(2.0 * M * (N // tp) * K for (_, N, K, _) in launch_lins) / n_lin
-        del codes
-    if tp == 1:  # the timed region itself: only the linear launches run in it (rank 0's)
-        t_g = ev0.elapsed_time(ev1) / 1e3 * a.roofline_reps / a.steps
-        per_launch_s = ev0.elapsed_time(ev1) / 1e3 / (a.steps * n_lin)
-    else:  # without the all-gathers
-        t_g, per_launch_s = graph_time(lambda: step(gather=False), n_lin)
-    bytes_launch = step_bytes / n_lin
+            def gemms():
+                for name, p in linears(stack):
+                    ops.gemm_w6ax(codes[name][0], codes[name][1], p["pk"], p["Nl"], p["abits"], out=p["out"])
+
+            _, per_gemm_s = ctx.graph_time(gemms, n_lin, a.roofline_reps)
+            ops_launch = layers * sum(2.0 * M * N * K for (_, N, K, _) in launch_lins) / n_lin
+            del codes
+        del stack, replay
+        torch.cuda.empty_cache()
+
     achieved = bytes_launch / per_launch_s / 1e9
     traffic, traffic_src = pmc_traffic(a.config, merge) if tp == 1 else (None, None)
-    if tp > 1:  # the same step without the all-gathers (max over ranks)
-        tg = torch.tensor([t_g / a.roofline_reps], dtype=torch.float64, device=dev)
-        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-        gemm_only_ms = float(tg.item()) * 1e3
-
     res = {
         "metric": "W6A6 GEMM TFLOPS-equiv + tok/s on LLaMA-2-7B linear shapes, 1/2/4/8 GPU",
         "value": round(value, 4),
@@ -430,13 +555,14 @@ def main():
             "workload": desc + ", dependent linear stack of every decoder layer per step",
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
-            "parallelism": (f"tp{world} column-parallel + RCCL all-gather per linear" if tp > 1 else
+            "parallelism": (f"tp{world}: every linear column-parallel (N/{world} rows per rank) + one RCCL "
+                            f"all-gather of its fp16 output per linear" if tp > 1 else
                             f"dp{world}: independent replicas, one token stream per GPU, no data-path collective"),
-            "graph": graph is not None,
-            "launches_per_layer": [[name, N, K, ab] for (name, N, K, ab) in launch_lins],
+            "graph": use_graph,
+            "launches_per_layer": [[name, N // tp, K, ab] for (name, N, K, ab) in launch_lins],
         },
         "roofline": {
-            "kernel": ("fq_gemm_decode_kernel<FUSE>" if all(fused.values()) else
+            "kernel": ("fq_gemm_decode_kernel<FUSE>" if fused_all else
                        "fq_gemm_decode_kernel (+ quantize where unfused)"),
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -448,13 +574,15 @@ def main():
             "traffic_over_alg": round(traffic / bytes_launch, 4) if traffic else None,
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
-            "fused_launches": all(fused.values()),
+            "fused_launches": fused_all,
             "method": ("HIP events on the launch stream around the timed steps (only the linear launches run)"
-                       if tp == 1 else "graph of the step's linear launches only (no all-gather), HIP events "
-                                          "on the capture stream"),
+                       if tp == 1 else "per rank: graph of the step's linear launches only (no all-gather), "
+                                       "HIP events on the capture stream; max over ranks"),
         },
     }
-    if prefill:
+    if staged:
+        res["rehearsal"] = "--share-gpu: all ranks on one GPU, gloo with host-staged gathers (not a valid result)"
+    if prefill and tp == 1:
         ach = ops_launch / per_gemm_s / 1e12
         res["roofline"] = {
             "kernel": "fq_gemm_prefill_kernel",
@@ -467,28 +595,49 @@ def main():
             "traffic_source": traffic_src,
             "per_launch_us": round(per_gemm_s * 1e6, 3),
             "alg_ops_per_launch": ops_launch,
-            "alg_bytes_per_launch": int(layers * sum(alg_bytes(M, N // tp, K, ab, False)
+            "alg_bytes_per_launch": int(layers * sum(alg_bytes(M, N, K, ab, False)
                                                      for (_, N, K, ab) in launch_lins) / n_lin),
             "step_ms_linears_incl_quantize": round(elapsed / a.steps * 1e3, 4),
             "method": "graph of the step's prefill GEMM launches on pre-quantized codes (the quantize "
                       "launches excluded), HIP events on the capture stream; TOPS = 2*M*N*K / launch time",
         }
     if tp > 1:
-        res["gemm_only_ms_per_step"] = round(gemm_only_ms, 4)
-        res["allgather_bytes_per_step_per_rank"] = int(layers * sum(2 * M * (N // world) * (world - 1)
-                                                                    for (_, N, K, _) in launch_lins))
+        res["tp"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()
+                     if k not in ("elapsed", "flops_step", "finite")}
+        res["tp"]["hbm_frac_per_rank"] = round(r["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)
+        if not a.no_replicas:  # the same model as independent replicas, one token stream per GPU
+            stack = build_stack(cfg, rank, 1, dev, merge)
+            replay = ctx.prepare(lambda: run_step(stack, M, 1), not a.no_graph)
+            el_dp, _ = ctx.timed(replay, a.steps, a.warmup)
+            res["replicas"] = {"what": f"dp{world}: the whole model on every GPU, independent token streams, "
+                                       "no data-path collective (weak scaling)",
+                               "value": round(world * flops_step * a.steps / el_dp / 1e12, 4),
+                               "tok_per_s": round(world * M * a.steps / el_dp, 2),
+                               "ms_per_step": round(el_dp / a.steps * 1e3, 4)}
+            del stack, replay
+            torch.cuda.empty_cache()
+        if not a.no_c4 and a.config != "llama2-70b-m1" and not prefill:
+            c4 = CONFIGS["llama2-70b-m1"]
+            rc = measure_tp(ctx, c4, merge, world, max(2, a.steps // 2), max(1, a.warmup // 2))
+            res["c4_llama2_70b_tp"] = {
+                "what": f"BASELINE config C4: {c4[3]}, column-parallel over {world} GPUs + one RCCL "
+                        f"all-gather per linear ({c4[0]} layers, {len(launch_list(c4[2], merge))} launches each)",
+                "value": round(rc["flops_step"] / (rc["ms_per_step"] / 1e3) / 1e12, 4),
+                "unit": "TFLOPS-equiv", "tok_per_s": round(1e3 / rc["ms_per_step"], 2),
+                **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in rc.items()
+                   if k not in ("elapsed", "flops_step")},
+                "hbm_frac_per_rank": round(rc["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
     if world == 1 and not a.no_calibrate:
         res["roofline"]["peak_measured"] = calibrate_peaks(dev)
         pm = res["roofline"]["peak_measured"]
         res["roofline"]["frac_of_measured"] = round(
             (ach / pm["int8_mfma_TOPS"]) if prefill else (achieved / pm["hbm_read_GBps"]), 4)
     if world == 1 and not a.no_fp16_compare:
-        del stack
         torch.cuda.empty_cache()
         shapes = sorted({(N, K) for (_, N, K, _) in lins})
         ab_cfg = max(ab for (_, _, _, ab) in lins)
         cmp_cfg = fp16_compare(shapes, M, ab_cfg, dev, reps=20 if not prefill else 4)
-        geo = lambda rows: round(float(np.exp(np.mean([np.log(r["speedup"]) for r in rows]))), 3)
+        geo = lambda rows: round(float(np.exp(np.mean([np.log(r["speedup"]) for r in rows]))), 3)  # noqa: E731
         res["vs_rocblas_fp16"] = {
             "what": f"W6A{ab_cfg} linear (quantize+GEMM, one launch where fused) vs torch F.linear fp16 "
                     "(hipBLASLt/rocBLAS), same M,N,K, graph-timed",

@@ -54,10 +54,25 @@ _SIGS = {
     "fq_import_ref_w": ([P, P, I, I, P, P], I),
     "fq_import_ref_x": ([P, P, I, I, I, P, P, P], I),
     "fq_bmma_scratch_bytes": ([I, I, I], SZ),
+    "fq_bmma_image_scratch_bytes": ([I, I, I], SZ),
     "fq_rmsnorm_quantize": ([P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),
     "fq_silu_mul_quantize": ([P, P, I, I, I, I, P, P, P, P], I),
 }
-EXPORTED = tuple(_SIGS) + ("fq_bmma_init", "fq_bmma_exec")
+
+
+class BmmaState(ctypes.Structure):
+    """fq_bmma_state (include/flexq_hip.h; FQBMMAOpState, flexq_bmma_op.h:19-34)."""
+    _fields_ = [("init_success", I), ("M", I), ("N", I), ("K", I), ("x_bits", I), ("w_bits", I),
+                ("group_size", I), ("w_format", I), ("prepared", I), ("X", P), ("W", P), ("X_SCALE", P),
+                ("W_SCALE", P), ("D", P), ("scratch", P), ("scratch_bytes", SZ)]
+
+
+_STRUCT_SIGS = {
+    "fq_bmma_init": ([P, P, P, P, I, I, I, P, I, I, I, I, P, SZ], BmmaState),
+    "fq_bmma_init_image": ([P, P, P, I, I, I, P, I, I, I, I, P, SZ], BmmaState),
+    "fq_bmma_exec": ([ctypes.POINTER(BmmaState), P], I),
+}
+EXPORTED = tuple(_SIGS) + tuple(_STRUCT_SIGS)
 
 _lib = None
 
@@ -74,7 +89,7 @@ def load():
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover - depends on the box
         raise FlexQExtensionError(f"failed to load {LIB_PATH}: {e}") from e
-    for name, (args, res) in _SIGS.items():
+    for name, (args, res) in list(_SIGS.items()) + list(_STRUCT_SIGS.items()):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

@@ -94,15 +94,20 @@ def load_image(path, device=None):
     return (t.to(device) if device is not None else t), meta
 
 
-def shard_parts(parts, tp_size, tp_rank, by_group=False):
+def shard_parts(parts, tp_size, tp_rank, by_group=False, return_offset=False):
     """Rows of this rank from each part of a fused linear, stacked: [part0_p; part1_p; ...].
-    by_group: rows split on 128-group boundaries (gate/up, matching down_proj's column split)."""
-    out = []
+    by_group: rows split on 128-group boundaries (gate/up, matching down_proj's column split).
+    With return_offset also the rank's row offset: the rows all lower ranks hold (the sum of the
+    parts' shard starts), i.e. where this file's rows begin when the ranks' files are stacked in
+    rank order -- exact for uneven group splits (11008 = 86 groups at TP 4: 22/22/21/21)."""
+    out, off = [], 0
     for w in parts:
         rng = group_shard_range if by_group else shard_range
         lo, hi = rng(w.shape[0], tp_size, tp_rank)
         out.append(w[lo:hi])
-    return torch.cat(out, 0).contiguous()
+        off += lo
+    stacked = torch.cat(out, 0).contiguous()
+    return (stacked, off) if return_offset else stacked
 
 
 def shard_columns(w, tp_size, tp_rank):
@@ -159,8 +164,8 @@ def convert_llama_safetensors(src, out_dir, tp_size=1, device="cuda:0", flex_dow
                 if split == ROW:
                     w_r, k_off = shard_columns(ws[0], tp_size, r)
                 else:
-                    w_r = shard_parts(ws, tp_size, r, by_group=fname == "mlp.gate_up_proj")
-                    row_off = r * w_r.shape[0]
+                    w_r, row_off = shard_parts(ws, tp_size, r, by_group=fname == "mlp.gate_up_proj",
+                                               return_offset=True)
                 img = pack_fp16(w_r, device)
                 path = os.path.join(out_dir, f"model.layers.{li}.{fname}.weight.{r}.fqw6")
                 save_image(path, img, w_r.shape[0], w_r.shape[1], abits, N_full=N_full, row_offset=row_off,

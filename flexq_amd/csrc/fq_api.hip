@@ -38,19 +38,26 @@ extern "C" fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int 
                         workspace_bytes, stream);
 }
 
-// ---- FQBMMAOpState-style interface over reference-layout activations -------------------------
+// ---- FQBMMAOpState-style interface (flexq_bmma_op.h:19-34,163-188) ---------------------------
+// scratch layout: [GEMM workspace (split-K tickets first) | weight image (bit-plane W only) |
+//                  xq int8 [M][K] | xs fp16 [K/128][M]], each 256-byte aligned.
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
-
-extern "C" size_t fq_bmma_scratch_bytes(int M, int N, int K) {
-    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
-    return align256((size_t)M * K) + align256((size_t)M * (K / FQ_GROUP) * 2) +
-           align256(fq_gemm_workspace_bytes(M, N, K));
+static size_t bmma_ws_bytes(int M, int N, int K) { return align256(fq_gemm_workspace_bytes(M, N, K)); }
+static size_t bmma_img_bytes(int N, int K, int w_format) {
+    return w_format == FQ_W_BITPLANES ? align256(fq_packed_w_bytes(N, K)) : 0;
 }
+static size_t bmma_x_bytes(int M, int K) { return align256((size_t)M * K) + align256((size_t)M * (K / FQ_GROUP) * 2); }
 
-extern "C" fq_bmma_state fq_bmma_init(const int32_t *X, const void *W, const uint16_t *X_SCALE,
-                                      const uint16_t *W_SCALE, int M, int N, int K, uint16_t *D,
-                                      int group_size, int bias, int x_bits, int w_bits,
-                                      void *scratch, size_t scratch_bytes) {
+static size_t bmma_scratch(int M, int N, int K, int w_format) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
+    return bmma_ws_bytes(M, N, K) + bmma_img_bytes(N, K, w_format) + bmma_x_bytes(M, K);
+}
+extern "C" size_t fq_bmma_scratch_bytes(int M, int N, int K) { return bmma_scratch(M, N, K, FQ_W_BITPLANES); }
+extern "C" size_t fq_bmma_image_scratch_bytes(int M, int N, int K) { return bmma_scratch(M, N, K, FQ_W_IMAGE); }
+
+static fq_bmma_state bmma_init(const int32_t *X, const void *W, int w_format, const uint16_t *X_SCALE,
+                               const uint16_t *W_SCALE, int M, int N, int K, uint16_t *D, int group_size,
+                               int bias, int x_bits, int w_bits, void *scratch, size_t scratch_bytes) {
     fq_bmma_state st = {};
     st.M = M;
     st.N = N;
@@ -58,6 +65,7 @@ extern "C" fq_bmma_state fq_bmma_init(const int32_t *X, const void *W, const uin
     st.x_bits = x_bits;
     st.w_bits = w_bits;
     st.group_size = group_size;
+    st.w_format = w_format;
     st.X = X;
     st.W = W;
     st.X_SCALE = X_SCALE;
@@ -65,25 +73,52 @@ extern "C" fq_bmma_state fq_bmma_init(const int32_t *X, const void *W, const uin
     st.D = D;
     st.scratch = scratch;
     st.scratch_bytes = scratch_bytes;
-    // Same acceptance rules as FQBMMAOp::initialize (flexq_bmma_op.h:81-133): group 128, no bias,
-    // K % 128 == 0; plus this build's W6 / A{6,8} and the bit-plane row rule (M <= 8 or M % 8 == 0).
-    // W is the weight image (fq_import_ref_w(W planes, W_SCALE) once, offline): it carries the
-    // group scales, so W_SCALE is kept for the signature and may be NULL.
-    st.init_success = X && W && X_SCALE && D && group_size == FQ_GROUP && !bias &&
-                      M > 0 && N > 0 && K > 0 && K % FQ_GROUP == 0 && (M <= 8 || M % 8 == 0) &&
-                      w_bits == 6 && (x_bits == 6 || x_bits == 8) && scratch &&
-                      scratch_bytes >= fq_bmma_scratch_bytes(M, N, K);
+    st.prepared = 0;
+    // FQBMMAOp::initialize's acceptance rules (flexq_bmma_op.h:81-133): group 128, no bias,
+    // K % 128 == 0; plus this build's W6 / A{6,8}, the bit-plane row rule (rows <= 8 or a multiple
+    // of 8, for X and -- in bit-plane form -- for W) and the scratch it needs.  Bit-plane W needs
+    // its W_SCALE (the reference reads it in every GEMM); an image already carries its scales.
+    const bool rows_ok = (M <= 8 || M % 8 == 0) && (w_format == FQ_W_IMAGE || N <= 8 || N % 8 == 0);
+    st.init_success = X && W && X_SCALE && D && (w_format == FQ_W_IMAGE || W_SCALE) &&
+                      group_size == FQ_GROUP && !bias && M > 0 && N > 0 && K > 0 && K % FQ_GROUP == 0 &&
+                      rows_ok && w_bits == 6 && (x_bits == 6 || x_bits == 8) && scratch &&
+                      scratch_bytes >= bmma_scratch(M, N, K, w_format) &&
+                      (size_t)((N + 15) / 16) <= 65536;
     return st;
 }
 
-extern "C" fq_status fq_bmma_exec(const fq_bmma_state *st, fq_stream_t stream) {
+extern "C" fq_bmma_state fq_bmma_init(const int32_t *X, const int32_t *W, const uint16_t *X_SCALE,
+                                      const uint16_t *W_SCALE, int M, int N, int K, uint16_t *D,
+                                      int group_size, int bias, int x_bits, int w_bits, void *scratch,
+                                      size_t scratch_bytes) {
+    return bmma_init(X, W, FQ_W_BITPLANES, X_SCALE, W_SCALE, M, N, K, D, group_size, bias, x_bits, w_bits,
+                     scratch, scratch_bytes);
+}
+
+extern "C" fq_bmma_state fq_bmma_init_image(const int32_t *X, const void *W_image, const uint16_t *X_SCALE,
+                                            int M, int N, int K, uint16_t *D, int group_size, int bias,
+                                            int x_bits, int w_bits, void *scratch, size_t scratch_bytes) {
+    return bmma_init(X, W_image, FQ_W_IMAGE, X_SCALE, nullptr, M, N, K, D, group_size, bias, x_bits, w_bits,
+                     scratch, scratch_bytes);
+}
+
+extern "C" fq_status fq_bmma_exec(fq_bmma_state *st, fq_stream_t stream) {
     if (!st || !st->init_success) return FQ_ERR_NULL;
     char *base = (char *)st->scratch;
-    int8_t *xq = (int8_t *)base;
-    uint16_t *xs = (uint16_t *)(base + align256((size_t)st->M * st->K));
-    void *ws = base + align256((size_t)st->M * st->K) + align256((size_t)st->M * (st->K / FQ_GROUP) * 2);
-    fq_status s = fq_import_ref_x(st->X, st->X_SCALE, st->M, st->K, st->x_bits, xq, xs, stream);
-    if (s != FQ_OK) return s;
-    return fq_gemm_w6ax(xq, xs, st->W, st->M, st->N, st->K, st->x_bits, st->D, nullptr,
-                        ws, fq_gemm_workspace_bytes(st->M, st->N, st->K), stream);
+    const size_t wsb = bmma_ws_bytes(st->M, st->N, st->K), imgb = bmma_img_bytes(st->N, st->K, st->w_format);
+    void *ws = base;
+    void *img = base + wsb;
+    int8_t *xq = (int8_t *)(base + wsb + imgb);
+    uint16_t *xs = (uint16_t *)(base + wsb + imgb + align256((size_t)st->M * st->K));
+    fq_status s;
+    if (!st->prepared) {  // first exec on this scratch: zero the ticket region, import W once
+        if ((s = fq_workspace_init(ws, wsb, stream)) != FQ_OK) return s;
+        if (st->w_format == FQ_W_BITPLANES &&
+            (s = fq_import_ref_w((const int32_t *)st->W, st->W_SCALE, st->N, st->K, img, stream)) != FQ_OK)
+            return s;
+        st->prepared = 1;
+    }
+    if ((s = fq_import_ref_x(st->X, st->X_SCALE, st->M, st->K, st->x_bits, xq, xs, stream)) != FQ_OK) return s;
+    return fq_gemm_w6ax(xq, xs, st->w_format == FQ_W_BITPLANES ? img : st->W, st->M, st->N, st->K, st->x_bits,
+                        st->D, nullptr, ws, fq_gemm_workspace_bytes(st->M, st->N, st->K), stream);
 }

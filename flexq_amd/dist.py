@@ -49,7 +49,12 @@ def gather_columns(local, group=None, out=None):
     world = dist.get_world_size(group)
     M, n = local.shape
     flat = torch.empty((world * M * n,), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(flat, local.contiguous().view(-1), group=group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":  # gloo: device tensors through the host
+        host = torch.empty((world * M * n,), dtype=local.dtype)
+        dist.all_gather_into_tensor(host, local.contiguous().view(-1).cpu(), group=group)
+        flat.copy_(host)
+    else:
+        dist.all_gather_into_tensor(flat, local.contiguous().view(-1), group=group)
     full = flat.view(world, M, n)
     if out is None:
         out = torch.empty((M, world * n), dtype=local.dtype, device=local.device)

@@ -50,20 +50,34 @@ def gemm_workspace_bytes(M, N, K):
 
 
 _WS = {}
+_WS_RETIRED = []  # superseded workspaces: a HIP graph captured earlier may still address them
 
 
 def workspace(device, nbytes, stream_handle):
-    """Per-(device, stream) scratch for the split-K fix-up (zeroed once, kept zero by the kernel)."""
+    """Per-(device, stream) scratch for the split-K fix-up and the prefill weight unpack (zeroed
+    once, the ticket region kept zero by the kernels).  Growing it never frees the old buffer:
+    graphs captured before the growth bake its address into their launches (split-K tickets and
+    slabs, the unpack image), so it stays allocated -- and its tickets zero -- for the process."""
     if nbytes == 0:
         return None
     key = (device, stream_handle)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         nbytes = max(nbytes, 1 << 20)
+        if buf is not None:
+            _WS_RETIRED.append(buf)
         buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
         _lib.call("fq_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
         _WS[key] = buf
     return buf
+
+
+def reserve_workspace(device, shapes, stream=None):
+    """Size the stream's workspace once for the largest of `shapes` [(M, N, K)] before any graph
+    capture (the way a serving loop would at start-up), so no later call grows it."""
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    nb = max((gemm_workspace_bytes(M, N, K) for (M, N, K) in shapes), default=0)
+    return workspace(torch.device(device), nb, s.cuda_stream)
 
 
 # ------------------------------------------------------------------------- weights

@@ -1,0 +1,192 @@
+/*
+ * flexq_gemm_wrapper.hpp -- header-only C++ drop-in for FlexQ's FLEXQGEMMWrapper
+ * (e2e/src/fastertransformer/kernels/flexqgemm/flexq_gemm_wrapper.h:6-48, .cu:9-122) over the C ABI
+ * of include/flexq_hip.h.  A FasterTransformer layer that holds a FLEXQGEMMWrapper
+ * (FfnLayer.cc:371-401, LlamaV2ContextAttentionLayer.cc:145-161) switches by changing the include
+ * and the namespace; the member signatures are the reference's, with hipStream_t for cudaStream_t.
+ *
+ *   FLEXQGEMMWrapper(X_BITS, W_BITS, SIGNED)  W6 with A6 or A8, SIGNED = true (the instantiated
+ *                                             families, flexq_bmma_library.cu:23-497)
+ *   pack(in, packed, x_scale, M, K, BIT, s)   = flexq_bit_packing(const half*...): quantize + bit
+ *                                             planes + duplicated x-scales (fq_ref_quantize_bit_packing)
+ *   gemm(M, N, K, const int* A, B, ...)       A = bit-plane activations from pack(), x_scale their
+ *                                             duplicated scales; B = bit-plane weights (W_BITS = 6),
+ *                                             w_scale = half[K/128][N] passed as float* (the
+ *                                             reference reinterprets it the same way, .cu:37-38)
+ *   gemm(M, N, K, const half* A, B, ...)      quantize + GEMM; at decode sizes ONE launch
+ *                                             (fq_linear_w6ax), x_scale is not written
+ *
+ * Differences, all host-side:
+ *   - B is imported into this build's weight image once per distinct B pointer (the image carries
+ *     W_SCALE), into device memory the wrapper owns and frees in its destructor; FT's weights are
+ *     loaded once and never rewritten.  set_weight_image(B, image) binds a caller-owned image
+ *     instead (no allocation), forget_weight(B) drops a binding after B is rewritten.
+ *   - The split-K tickets / slabs and the prefill unpack buffer live in a wrapper-owned, zeroed
+ *     device workspace (grown, never shrunk, superseded buffers kept until destruction, so a
+ *     captured graph never addresses freed memory).  flexq_gemm_workspace holds only the
+ *     activation codes: workspace_bytes(M, N, K) bytes (the reference asks 6*M*maxK/8,
+ *     LlamaV2ContextAttentionLayer.cc:793; here 2*M*K + M*K/64 + alignment, the first M*K of it
+ *     left to the caller's pack() output exactly like the reference's half path, .cu:118).
+ *   - C (bias), scale_inter and scale_out are unused, as in the reference (bias = true is rejected
+ *     by FQBMMAOp::initialize, flexq_bmma_op.h:103-126).
+ * Errors are printed as "[FlexQ][Error] ..." and the call returns, like the reference
+ * (.cu:44,88,93); status() holds the last fq_status for callers that want to check.
+ */
+#pragma once
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <unordered_map>
+#include <vector>
+
+#include "flexq_hip.h"
+
+namespace flexq_amd {
+
+class FLEXQGEMMWrapper {
+  public:
+    FLEXQGEMMWrapper(int X_BITS, int W_BITS, bool SIGNED) : x_bits_(X_BITS), w_bits_(W_BITS), signed_(SIGNED) {}
+    ~FLEXQGEMMWrapper() {
+        for (auto &kv : images_)
+            if (kv.second.owned) (void)hipFree(kv.second.ptr);
+        for (void *p : workspaces_) (void)hipFree(p);
+        release_retired();
+    }
+    FLEXQGEMMWrapper(const FLEXQGEMMWrapper &) = delete;
+    FLEXQGEMMWrapper &operator=(const FLEXQGEMMWrapper &) = delete;
+
+    /* caller workspace (flexq_gemm_workspace) for gemm() at this shape */
+    static size_t workspace_bytes(int M, int N, int K) {
+        (void)N;
+        return 2 * align((size_t)M * K) + align((size_t)M * (K / 128) * 2);
+    }
+
+    void pack(const half *in_data, int *packed_data, half *x_scale, int M, int K, int BIT, hipStream_t stream) {
+        report(fq_ref_quantize_bit_packing(reinterpret_cast<const uint16_t *>(in_data), packed_data,
+                                           reinterpret_cast<uint16_t *>(x_scale), M, K, BIT, (fq_stream_t)stream),
+               "pack");
+    }
+
+    void gemm(const int M, const int N, const int K, const int *A, const int *B, const half *C, half *D,
+              float *x_scale, const float *w_scale, const float *scale_inter, const float *scale_out, bool bias,
+              char *flexq_gemm_workspace, size_t flexq_gemm_ws_bytes, hipStream_t stream = nullptr) {
+        (void)C, (void)scale_inter, (void)scale_out;
+        if (!check(M, N, K, bias, flexq_gemm_workspace, flexq_gemm_ws_bytes)) return;
+        const void *img = image_for(B, reinterpret_cast<const uint16_t *>(w_scale), N, K, stream);
+        if (!img) return;
+        int8_t *xq = reinterpret_cast<int8_t *>(flexq_gemm_workspace + align((size_t)M * K));
+        uint16_t *xs = reinterpret_cast<uint16_t *>(flexq_gemm_workspace + 2 * align((size_t)M * K));
+        if (!report(fq_import_ref_x(A, reinterpret_cast<const uint16_t *>(x_scale), M, K, x_bits_, xq, xs,
+                                    (fq_stream_t)stream),
+                    "gemm: activation import"))
+            return;
+        void *ws = gemm_workspace(M, N, K, stream);
+        if (!ws && fq_gemm_workspace_bytes(M, N, K)) return;
+        report(fq_gemm_w6ax(xq, xs, img, M, N, K, x_bits_, reinterpret_cast<uint16_t *>(D), nullptr, ws,
+                            ws_bytes_, (fq_stream_t)stream),
+               "gemm");
+    }
+
+    void gemm(const int M, const int N, const int K, const half *A, const int *B, const half *C, half *D,
+              float *x_scale, const float *w_scale, const float *scale_inter, const float *scale_out, bool bias,
+              char *flexq_gemm_workspace, size_t flexq_gemm_ws_bytes, hipStream_t stream = nullptr) {
+        (void)C, (void)x_scale, (void)scale_inter, (void)scale_out;
+        if (!check(M, N, K, bias, flexq_gemm_workspace, flexq_gemm_ws_bytes)) return;
+        const void *img = image_for(B, reinterpret_cast<const uint16_t *>(w_scale), N, K, stream);
+        if (!img) return;
+        int8_t *xq = reinterpret_cast<int8_t *>(flexq_gemm_workspace + align((size_t)M * K));
+        uint16_t *xs = reinterpret_cast<uint16_t *>(flexq_gemm_workspace + 2 * align((size_t)M * K));
+        void *ws = gemm_workspace(M, N, K, stream);
+        if (!ws && fq_gemm_workspace_bytes(M, N, K)) return;
+        report(fq_linear_w6ax(reinterpret_cast<const uint16_t *>(A), M, N, K, x_bits_, img,
+                              reinterpret_cast<uint16_t *>(D), xq, xs, ws, ws_bytes_, (fq_stream_t)stream),
+               "gemm");
+    }
+
+    /* bind a caller-owned weight image (fq_import_ref_w / fq_pack_w6 output) to the pointer B */
+    void set_weight_image(const int *B, const void *image) { images_[B] = Image{const_cast<void *>(image), false}; }
+    void forget_weight(const int *B) {
+        auto it = images_.find(B);
+        if (it == images_.end()) return;
+        if (it->second.owned) retired_images_.push_back(it->second.ptr);  // a graph may still read it
+        images_.erase(it);
+    }
+    fq_status status() const { return last_; }
+
+  private:
+    struct Image {
+        void *ptr;
+        bool owned;
+    };
+    static size_t align(size_t v) { return (v + 255) & ~(size_t)255; }
+
+    bool report(fq_status s, const char *what) {
+        last_ = s;
+        if (s != FQ_OK) fprintf(stderr, "[FlexQ][Error] %s: %s\n", what, fq_status_string(s));
+        return s == FQ_OK;
+    }
+
+    bool check(int M, int N, int K, bool bias, char *ws, size_t ws_bytes) {
+        if (K < 128 || K % 128 != 0) return report(FQ_ERR_SHAPE, "unsupported K");  // .cu:43-46
+        if (w_bits_ != 6 || (x_bits_ != 6 && x_bits_ != 8) || !signed_) return report(FQ_ERR_BITS, "unsupported w/a bits");
+        if (M <= 0 || N <= 0) return report(FQ_ERR_SHAPE, "unsupported M/N");
+        if (bias) return report(FQ_ERR_SHAPE, "bias is not supported (FQBMMAOp::initialize)");
+        if (!ws || ws_bytes < workspace_bytes(M, N, K)) return report(FQ_ERR_WORKSPACE, "flexq_gemm_workspace too small");
+        return true;
+    }
+
+    const void *image_for(const int *B, const uint16_t *w_scale, int N, int K, hipStream_t stream) {
+        auto it = images_.find(B);
+        if (it != images_.end()) return it->second.ptr;
+        void *img = nullptr;
+        if (hipMalloc(&img, fq_packed_w_bytes(N, K)) != hipSuccess) {
+            report(FQ_ERR_HIP, "weight image allocation");
+            return nullptr;
+        }
+        if (!report(fq_import_ref_w(B, w_scale, N, K, img, (fq_stream_t)stream), "weight import")) {
+            (void)hipFree(img);
+            return nullptr;
+        }
+        images_[B] = Image{img, true};
+        return img;
+    }
+
+    void *gemm_workspace(int M, int N, int K, hipStream_t stream) {
+        const size_t need = fq_gemm_workspace_bytes(M, N, K);
+        if (need <= ws_bytes_) return ws_;
+        void *p = nullptr;
+        if (hipMalloc(&p, need) != hipSuccess) {
+            report(FQ_ERR_HIP, "gemm workspace allocation");
+            return nullptr;
+        }
+        if (!report(fq_workspace_init(p, need, (fq_stream_t)stream), "gemm workspace init")) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        workspaces_.push_back(p);  // the old one stays allocated until destruction
+        ws_ = p;
+        ws_bytes_ = need;
+        return ws_;
+    }
+
+    int x_bits_, w_bits_;
+    bool signed_;
+    fq_status last_ = FQ_OK;
+    std::unordered_map<const int *, Image> images_;
+    std::vector<void *> retired_images_;
+    std::vector<void *> workspaces_;
+    void *ws_ = nullptr;
+    size_t ws_bytes_ = 0;
+
+  public:
+    /* free images dropped by forget_weight() (once no captured graph reads them; the destructor
+     * frees them too) */
+    void release_retired() {
+        for (void *p : retired_images_) (void)hipFree(p);
+        retired_images_.clear();
+    }
+};
+
+}  // namespace flexq_amd

@@ -158,29 +158,49 @@ fq_status fq_import_ref_w(const int32_t *w_bitplanes, const uint16_t *w_scale, i
 fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, int M, int K,
                           int bits, int8_t *xq, uint16_t *xs, fq_stream_t stream);
 
-/* FQBMMAOpState-style two-call interface over REFERENCE-layout operands
- * (flexq_bmma_op.h:19-34,163-188): init validates and records the arguments (no launch, no
- * device-attribute call per init, unlike flexq_bmma_op.h:103), exec imports X from bit planes
- * into `scratch` and runs fq_gemm_w6ax.  W must already be a weight image (import it once with
- * fq_import_ref_w(W planes, W_SCALE), as FT loads pre-packed weights once); the image carries
- * the scales, so W_SCALE is recorded but not read (may be NULL).  scratch: fq_bmma_scratch_bytes(). */
+/* FQBMMAOpState-style two-call interface (flexq_bmma_op.h:19-34, FQBMMAInitFn_t / FQBMMAExecFn_t
+ * at :187-188): init validates and records the arguments -- no launch, and no device-attribute
+ * call per init (unlike flexq_bmma_op.h:103) -- and exec runs the GEMM.
+ *
+ * fq_bmma_init takes the REFERENCE operands: X and W as bit planes (fq_ref_bit_packing layout,
+ * W_BITS = 6) with X_SCALE in the reference's duplicated layout and W_SCALE half[K/128][N]
+ * (required).  The first fq_bmma_exec on a state zeroes the scratch's ticket region and imports
+ * W + W_SCALE into a weight image inside `scratch` (once: FT loads its weights once, and
+ * `prepared` records it; set it back to 0 after rewriting W); every exec imports X from its bit
+ * planes and runs fq_gemm_w6ax.  Run the first exec eagerly before capturing a graph.
+ * fq_bmma_init_image is the fast path for callers that keep the weight image (fq_import_ref_w /
+ * fq_pack_w6 output) themselves: no W_SCALE, no image in scratch.  A caller cannot pass one form
+ * for the other by accident: the two entry points name the form.
+ * Rejections (init_success = 0, like FQBMMAOp::initialize): NULL operands, group_size != 128,
+ * bias, K % 128, W_BITS != 6, X_BITS not 6/8, bit-plane rows (M, and N for bit-plane W) neither
+ * <= 8 nor a multiple of 8, scratch smaller than fq_bmma_scratch_bytes / _image_scratch_bytes.
+ * The caller's scratch needs no initialisation. */
+#define FQ_W_BITPLANES 0 /* reference bit planes + W_SCALE */
+#define FQ_W_IMAGE 1     /* this build's weight image */
 typedef struct fq_bmma_state {
     int init_success;
     int M, N, K, x_bits, w_bits, group_size;
+    int w_format;            /* FQ_W_BITPLANES or FQ_W_IMAGE */
+    int prepared;            /* set by the first exec: tickets zeroed, W imported */
     const int32_t *X;        /* reference bit-plane activations */
-    const void *W;           /* weight image */
-    const uint16_t *X_SCALE; /* reference duplicated layout */
-    const uint16_t *W_SCALE; /* [K/128][N], not read (the image carries the scales) */
-    uint16_t *D;
+    const void *W;           /* bit planes (FQ_W_BITPLANES) or a weight image (FQ_W_IMAGE) */
+    const uint16_t *X_SCALE; /* reference duplicated layout half[K/128][2*ceil4(M)] */
+    const uint16_t *W_SCALE; /* half[K/128][N] (FQ_W_BITPLANES) */
+    uint16_t *D;             /* half[M][N] */
     void *scratch;
     size_t scratch_bytes;
 } fq_bmma_state;
 size_t fq_bmma_scratch_bytes(int M, int N, int K);
-fq_bmma_state fq_bmma_init(const int32_t *X, const void *W, const uint16_t *X_SCALE,
+size_t fq_bmma_image_scratch_bytes(int M, int N, int K);
+fq_bmma_state fq_bmma_init(const int32_t *X, const int32_t *W, const uint16_t *X_SCALE,
                            const uint16_t *W_SCALE, int M, int N, int K, uint16_t *D,
                            int group_size, int bias, int x_bits, int w_bits, void *scratch,
                            size_t scratch_bytes);
-fq_status fq_bmma_exec(const fq_bmma_state *state, fq_stream_t stream);
+fq_bmma_state fq_bmma_init_image(const int32_t *X, const void *W_image, const uint16_t *X_SCALE,
+                                 int M, int N, int K, uint16_t *D, int group_size, int bias,
+                                 int x_bits, int w_bits, void *scratch, size_t scratch_bytes);
+/* FQBMMAExecFn_t(FQBMMAOpState&, stream): the state is updated (prepared) on the first call. */
+fq_status fq_bmma_exec(fq_bmma_state *state, fq_stream_t stream);
 
 #ifdef __cplusplus
 }

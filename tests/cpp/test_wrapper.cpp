@@ -1,0 +1,124 @@
+// test_wrapper.cpp -- drives include/flexq_gemm_wrapper.hpp (the FLEXQGEMMWrapper drop-in) the way
+// a FasterTransformer layer does (FfnLayer.cc:371-401): weights as reference bit planes + W_SCALE,
+// gemm(const half* A ...) for quantize + GEMM, and pack() + gemm(const int* A ...) for the
+// two-step form.  It writes its inputs and both outputs to <outdir> as raw little-endian files;
+// tests/test_gpu_wrapper.py checks them against the CPU oracle.  Test infrastructure only.
+//
+// usage: test_wrapper <outdir> <M> <N> <K> <abits> <seed>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "flexq_gemm_wrapper.hpp"
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(2);                                                                  \
+        }                                                                             \
+    } while (0)
+
+static uint64_t g_state;
+static uint32_t next_u32() {  // splitmix64
+    uint64_t z = (g_state += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+static float uniform() { return (next_u32() >> 8) * (1.0f / 16777216.0f); }
+
+template <class T>
+static void dump(const std::string &path, const std::vector<T> &v) {
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f || fwrite(v.data(), sizeof(T), v.size(), f) != v.size()) {
+        fprintf(stderr, "cannot write %s\n", path.c_str());
+        exit(2);
+    }
+    fclose(f);
+}
+
+int main(int argc, char **argv) {
+    if (argc != 7) {
+        fprintf(stderr, "usage: %s outdir M N K abits seed\n", argv[0]);
+        return 2;
+    }
+    const std::string out = argv[1];
+    const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), abits = atoi(argv[5]);
+    g_state = strtoull(argv[6], nullptr, 10);
+    if (M <= 0 || N <= 0 || K <= 0 || K % 128 || (N > 8 && N % 8) || (M > 8 && M % 8) || (abits != 6 && abits != 8)) {
+        fprintf(stderr, "unsupported case\n");
+        return 2;
+    }
+    // host inputs: activations ~ U(-2, 2) with a few outliers, raw 6-bit weight patterns,
+    // weight scales U(0, 0.05)
+    std::vector<__half> x((size_t)M * K);
+    for (size_t i = 0; i < x.size(); i++) x[i] = __float2half((uniform() * 4.f - 2.f) * (i % 97 == 0 ? 16.f : 1.f));
+    std::vector<int32_t> wraw((size_t)N * K);
+    for (auto &v : wraw) v = (int32_t)(next_u32() & 63);
+    std::vector<__half> ws((size_t)(K / 128) * N);
+    for (auto &v : ws) v = __float2half(uniform() * 0.05f);
+
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    __half *dx, *dws, *dd1, *dd2, *dxs;
+    int32_t *dwraw, *dwp, *dxp;
+    char *dwork;
+    const size_t wpb = (size_t)6 * N * (K / 32) * 4, xpb = (size_t)abits * M * (K / 32) * 4;
+    const size_t xsdup = (size_t)(K / 128) * 2 * ((M + 3) / 4 * 4) * 2;
+    const size_t work = flexq_amd::FLEXQGEMMWrapper::workspace_bytes(M, N, K);
+    CK(hipMalloc(&dx, x.size() * 2));
+    CK(hipMalloc(&dws, ws.size() * 2));
+    CK(hipMalloc(&dd1, (size_t)M * N * 2));
+    CK(hipMalloc(&dd2, (size_t)M * N * 2));
+    CK(hipMalloc(&dxs, xsdup));
+    CK(hipMalloc(&dwraw, wraw.size() * 4));
+    CK(hipMalloc(&dwp, wpb));
+    CK(hipMalloc(&dxp, xpb));
+    CK(hipMalloc(&dwork, work));
+    CK(hipMemcpy(dx, x.data(), x.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dws, ws.data(), ws.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dwraw, wraw.data(), wraw.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(dwork, 0xA5, work));  // the caller's workspace needs no initialisation
+    // the weights as FT holds them: bit planes (flexq_bit_packing on the raw patterns)
+    if (fq_ref_bit_packing(dwraw, dwp, N, K, 6, (fq_stream_t)s) != FQ_OK) return 3;
+
+    flexq_amd::FLEXQGEMMWrapper w(abits, 6, true);
+    // 1. gemm(const half* A ...): quantize + GEMM (one launch at decode sizes)
+    w.gemm(M, N, K, dx, dwp, nullptr, dd1, reinterpret_cast<float *>(dxs), reinterpret_cast<const float *>(dws),
+           nullptr, nullptr, false, dwork, work, s);
+    if (w.status() != FQ_OK) return 4;
+    // 2. pack() into the workspace's head, then gemm(const int* A ...), as the reference's half
+    //    path does internally (flexq_gemm_wrapper.cu:99-122)
+    w.pack(dx, dxp, dxs, M, K, abits, s);
+    if (w.status() != FQ_OK) return 5;
+    for (int rep = 0; rep < 2; rep++) {  // the second call reuses the imported weight image
+        w.gemm(M, N, K, dxp, dwp, nullptr, dd2, reinterpret_cast<float *>(dxs), reinterpret_cast<const float *>(dws),
+               nullptr, nullptr, false, dwork, work, s);
+        if (w.status() != FQ_OK) return 6;
+    }
+    // 3. the reference's rejections print and return
+    w.gemm(M, N, 100, dx, dwp, nullptr, dd1, nullptr, nullptr, nullptr, nullptr, false, dwork, work, s);
+    if (w.status() != FQ_ERR_SHAPE) return 7;
+    w.gemm(M, N, K, dx, dwp, nullptr, dd1, nullptr, nullptr, nullptr, nullptr, false, dwork, 16, s);
+    if (w.status() != FQ_ERR_WORKSPACE) return 8;
+    CK(hipStreamSynchronize(s));
+
+    std::vector<__half> d1((size_t)M * N), d2((size_t)M * N);
+    CK(hipMemcpy(d1.data(), dd1, d1.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(d2.data(), dd2, d2.size() * 2, hipMemcpyDeviceToHost));
+    dump(out + "/x.f16", x);
+    dump(out + "/wraw.i32", wraw);
+    dump(out + "/ws.f16", ws);
+    dump(out + "/d_half.f16", d1);
+    dump(out + "/d_int.f16", d2);
+    for (void *p : {(void *)dx, (void *)dws, (void *)dd1, (void *)dd2, (void *)dxs, (void *)dwraw, (void *)dwp,
+                    (void *)dxp, (void *)dwork})
+        CK(hipFree(p));
+    CK(hipStreamDestroy(s));
+    printf("test_wrapper ok M=%d N=%d K=%d a%d\n", M, N, K, abits);
+    return 0;
+}

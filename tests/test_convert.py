@@ -64,3 +64,19 @@ def test_row_parallel_columns_and_matching_gate_rows():
         assert rows.shape[0] == 2 * cols.shape[1]
         assert rows[:cols.shape[1], 0].tolist() == list(range(k_off, k_off + cols.shape[1]))
         assert torch.equal(cols, down[:, k_off:k_off + cols.shape[1]])
+
+
+def test_uneven_group_shards_have_cumulative_row_offsets():
+    """LLaMA-2-7B gate/up at TP 4: 11008 = 86 groups -> 22/22/21/21 groups per rank.  Each rank's
+    stacked [gate_p; up_p] file starts where the lower ranks' files end."""
+    F, P = 11008, 4
+    gate = torch.arange(F).view(F, 1)
+    up = F + torch.arange(F).view(F, 1)
+    offs, sizes = [], []
+    for r in range(P):
+        rows, off = convert.shard_parts([gate, up], P, r, by_group=True, return_offset=True)
+        offs.append(off)
+        sizes.append(rows.shape[0])
+    assert sizes == [2 * 22 * 128, 2 * 22 * 128, 2 * 21 * 128, 2 * 21 * 128]
+    assert offs == [0, sizes[0], sizes[0] + sizes[1], sizes[0] + sizes[1] + sizes[2]]
+    assert sum(sizes) == 2 * F

@@ -1,0 +1,213 @@
+"""GPU parity against the REFERENCE-generated golden vectors (tests/golden/*.npz).
+
+The fixtures were produced by importing the reference's own `algorithm/flexq_quantize`
+(`tests/golden/gen_golden.py`: UniformAffineQuantizer, quantizer.py:128-171; QuantLinear,
+int_linear.py:56-72) on the seeded inputs `tests/golden/inputs.py` regenerates bit for bit.  Here
+those inputs go through the HIP path (fq_quantize_act, fq_quantize_pack_w6, fq_linear_w6ax and
+the operator surface's QuantLinear.to_engine()) and the results are held against the reference's
+numbers directly -- no restatement in between:
+
+* scales: the engine rule half(absmax_f32 / (2^(b-1)-1)) and the reference's fp16
+  `clamp(absmax / qmax, 1e-5, 1e4)` coincide bit for bit on every group where the
+  reference's 1e-5 floor is inactive; the floored groups (all-zero / tiny) are derived and checked
+  separately.
+* codes: equal everywhere except where the two rounding rules provably part -- the reference
+  rounds half-to-even on the fp16-rounded quotient, the engine rounds half away from zero on the
+  fp32 quotient.  That mask is computed here from the golden scale and the input alone (not from
+  the HIP output); inside it the HIP code must be the engine rule's value and differ by one.
+* QuantLinear outputs (C1: M = 1, K = N = 4096, W6A6; M = 16 W6A8): the HIP output is within the
+  exact bound that the masked code differences imply, plus the fp16 noise of the reference's own
+  CPU F.linear, of the golden y.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from inputs import act_input, edge_inputs, weight_input
+
+from flexq_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+F16_FLOOR = np.float32(np.float16(1e-5))  # the reference's scale clamp(min=1e-5) in fp16
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+def rule_split(x16, scale_groups, bits):
+    """Per element: (reference code, engine code) from the input and the GOLDEN per-group scale.
+    x16 fp16 [R, K]; scale_groups fp16 [R*K/128] (row-major groups, the reference's order)."""
+    R, K = x16.shape
+    hi = (1 << (bits - 1)) - 1
+    sc = np.repeat(scale_groups.astype(np.float32).reshape(R, K // 128), 128, axis=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q32 = x16.astype(np.float32) / sc
+    ref = np.clip(np.rint(q32.astype(np.float16).astype(np.float32)), -hi - 1, hi)
+    eng = np.clip(np.sign(q32) * np.floor(np.abs(q32) + np.float32(0.5)), -hi - 1, hi)
+    # 0 / 0 (a zero in a group whose scale underflowed to 0): the saturating convert gives 0
+    return ref, np.nan_to_num(eng, nan=0.0)
+
+
+def floored_groups(x16, bits):
+    """Groups where the reference's 1e-5 scale floor is active: absmax/qmax < 1e-5 in fp16."""
+    R, K = x16.shape
+    hi = (1 << (bits - 1)) - 1
+    amax = np.abs(x16.astype(np.float32)).reshape(R, K // 128, 128).max(-1).reshape(-1)
+    return (amax / np.float32(hi)).astype(np.float16).astype(np.float32) < F16_FLOOR
+
+
+def hip_quantize(x16, bits, dev):
+    xq, xs = ops.quantize_act(torch.from_numpy(x16).to(dev), bits)
+    torch.cuda.synchronize()
+    return xq.cpu().numpy(), xs.cpu().numpy().T.reshape(-1)  # xs [K/128, M] -> reference group order
+
+
+def check_against_golden(x16, bits, g_scale, g_codes, dev, max_frac):
+    R, K = x16.shape
+    xq, xs = hip_quantize(x16, bits, dev)
+    g_scale = g_scale.reshape(-1)
+    floor = floored_groups(x16, bits)
+    # 1. scales: bit-exact wherever the reference's floor is inactive
+    np.testing.assert_array_equal(xs[~floor].view(np.uint16), g_scale[~floor].view(np.uint16))
+    # the floored groups: the reference holds the floor, the engine the unfloored quotient
+    assert np.all(g_scale[floor].astype(np.float32) == F16_FLOOR)
+    amax = np.abs(x16.astype(np.float32)).reshape(-1, 128).max(-1)
+    hi = (1 << (bits - 1)) - 1
+    np.testing.assert_array_equal(xs[floor].view(np.uint16),
+                                  (amax[floor] / np.float32(hi)).astype(np.float16).view(np.uint16))
+    # 2. codes: golden codes are [R*K/128, 128] row-major groups
+    ncodes = g_codes.shape[0]
+    hip_codes = xq.reshape(-1, 128)[:ncodes].astype(np.int32)
+    ref_codes = g_codes.astype(np.int32)
+    ref_rule, eng_rule = rule_split(x16, g_scale, bits)
+    ref_rule = ref_rule.reshape(-1, 128)[:ncodes]
+    eng_rule = eng_rule.reshape(-1, 128)[:ncodes]
+    gfloor = np.repeat(floor[:ncodes], 128).reshape(-1, 128)
+    # the derivation reproduces the reference's own codes outside floored groups
+    np.testing.assert_array_equal(ref_rule[~gfloor], ref_codes[~gfloor])
+    mask = (ref_rule != eng_rule) & ~gfloor
+    np.testing.assert_array_equal(hip_codes[~mask & ~gfloor], ref_codes[~mask & ~gfloor])
+    np.testing.assert_array_equal(hip_codes[mask], eng_rule[mask])
+    assert np.all(np.abs(hip_codes[mask] - ref_codes[mask]) == 1)
+    assert mask.mean() <= max_frac, f"{mask.mean():.4f} of codes on a rounding-rule boundary"
+    # floored groups: the engine's codes are its own rule on its own (unfloored) scale
+    if gfloor.any():
+        _, eng_own = rule_split(x16, xs, bits)
+        eng_own = eng_own.reshape(-1, 128)[:ncodes]
+        zero_groups = (amax[:ncodes] == 0)
+        np.testing.assert_array_equal(hip_codes[gfloor & ~np.repeat(zero_groups, 128).reshape(-1, 128)],
+                                      eng_own[gfloor & ~np.repeat(zero_groups, 128).reshape(-1, 128)])
+        assert np.all(hip_codes[np.repeat(zero_groups, 128).reshape(-1, 128)] == 0)
+    return mask.mean()
+
+
+@pytest.mark.parametrize("bits", [6, 8])
+def test_activation_quantizer_vs_reference_fixture(dev, bits):
+    g = gold(f"act_fp16_a{bits}.npz")
+    x16 = act_input(16, 1024, seed=11 + bits).astype(np.float16)
+    frac = check_against_golden(x16, bits, g["scale"], g["codes"], dev, 0.01 if bits == 6 else 0.03)
+    # and the fake-quant x_hat the reference stores agrees with the engine codes x scale outside
+    # the mask (x_hat = fp16(code * scale))
+    assert frac < 0.03
+
+
+@pytest.mark.parametrize("case", ["zero", "ties", "outlier", "tiny", "three_d"])
+@pytest.mark.parametrize("bits", [6, 8])
+def test_edge_groups_vs_reference_fixture(dev, case, bits):
+    g = gold("edge_fp16.npz")
+    x = edge_inputs()[case]
+    x16 = x.reshape(-1, x.shape[-1]).astype(np.float16)
+    # ties sit exactly on .5 of the scale: the whole point of the mask (half-even vs half-away)
+    max_frac = 0.6 if case == "ties" else 0.03
+    check_against_golden(x16, bits, g[f"{case}_a{bits}_scale"], g[f"{case}_a{bits}_codes"], dev, max_frac)
+
+
+def test_weight_quantizer_vs_reference_fixture(dev):
+    """fq_quantize_pack_w6 (the engine's offline weight quantizer) against the reference's
+    weight_quant_inplace on the same fp16 weight: scales bit-exact, codes outside the mask."""
+    g = gold("wq_fp16.npz")
+    w16 = weight_input(64, 512, seed=7).astype(np.float16)
+    wpk, ws, wq = ops.quantize_pack_w6(torch.from_numpy(w16).to(dev), return_codes=True)
+    torch.cuda.synchronize()
+    ws = ws.cpu().numpy().T.reshape(-1)  # [K/128, N] -> (row, group) order
+    np.testing.assert_array_equal(ws.view(np.uint16), g["scale"].reshape(-1).view(np.uint16))
+    ref_rule, eng_rule = rule_split(w16, g["scale"], 6)
+    codes = wq.cpu().numpy().reshape(-1, 128).astype(np.int32)
+    gc = g["codes"].astype(np.int32)
+    mask = (ref_rule != eng_rule).reshape(-1, 128)[:gc.shape[0]]
+    np.testing.assert_array_equal(codes[:gc.shape[0]][~mask], gc[~mask])
+    assert mask.mean() <= 0.01
+    # the image round-trips to the same codes and scales
+    wq2, ws2 = ops.unpack_w6(wpk, 64, 512)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(wq2.cpu().numpy(), wq.cpu().numpy())
+
+
+def linear_bound(x16, w16, xs_g, ws_g, abits):
+    """Exact float64 product under the reference's codes, and the bound the masked code
+    differences imply: |sum_k (q_ref - q_eng)_k * xs * w_hat_k|."""
+    M, K = x16.shape
+    N = w16.shape[0]
+    ref_x, eng_x = rule_split(x16, xs_g, abits)
+    ref_w, eng_w = rule_split(w16, ws_g, 6)
+    sx = np.repeat(xs_g.astype(np.float64).reshape(M, K // 128), 128, axis=1)
+    sw = np.repeat(ws_g.astype(np.float64).reshape(N, K // 128), 128, axis=1)
+    xh, wh = ref_x * sx, ref_w * sw
+    y_exact = xh @ wh.T
+    absdot = np.abs(xh) @ np.abs(wh).T
+    bound = np.abs((ref_x - eng_x) * sx) @ np.abs(eng_w * sw).T + np.abs(xh) @ np.abs((ref_w - eng_w) * sw).T
+    return y_exact, absdot, bound
+
+
+@pytest.mark.parametrize("tag,M,K,N,abits", [("m1", 1, 4096, 4096, 6), ("m16a8", 16, 1024, 256, 8)])
+@pytest.mark.parametrize("surface", ["c_abi", "quantlinear"])
+def test_quant_linear_vs_reference_fixture(dev, tag, M, K, N, abits, surface):
+    """C1 (M = 1, K = N = 4096, W6A6) and the M = 16 W6A8 down_proj case against the reference's
+    QuantLinear.forward outputs: through fq_linear_w6ax directly and through the operator surface
+    (QuantLinear(...).to_engine()), the reference flow's weight_quant_inplace included."""
+    g = gold(f"linear_fp16_{tag}.npz")
+    x16 = act_input(M, K, seed=2).astype(np.float16)
+    w16 = weight_input(N, K, seed=1).astype(np.float16)
+    x = torch.from_numpy(x16).to(dev)
+    if surface == "c_abi":
+        wpk, ws = ops.quantize_pack_w6(torch.from_numpy(w16).to(dev))
+        np.testing.assert_array_equal(ws.cpu().numpy().T.reshape(-1).view(np.uint16),
+                                      g["w_scale"].reshape(-1).view(np.uint16))
+        y = ops.linear_w6ax(x, wpk, N, abits)
+    else:
+        import torch.nn as nn
+        from flexq_amd.flexq_quantize import QuantLinear, register_scales_and_zeros, set_quant_state, \
+            weight_quant_inplace
+        lin = nn.Linear(K, N, bias=False)
+        lin.weight.data = torch.from_numpy(w16.copy())
+        wp = dict(n_bits=6, per_channel_axes=[0], symmetric=True, dynamic_method="per_group",
+                  group_size=128, disable_zero_point=True)
+        ap = dict(n_bits=abits, per_channel_axes=[], symmetric=True, dynamic_method="per_group",
+                  group_size=128, disable_zero_point=True)
+        ql = QuantLinear(lin, wp, ap).to(dev)
+        set_quant_state(ql, True, True)
+        weight_quant_inplace(ql)
+        register_scales_and_zeros(ql)
+        np.testing.assert_array_equal(ql.weight_quantizer.scales.cpu().numpy().reshape(-1).view(np.uint16),
+                                      g["w_scale"].reshape(-1).view(np.uint16))
+        with torch.no_grad():
+            y = ql.to_engine()(x)
+    xq, xs = ops.quantize_act(x, abits)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(xs.cpu().numpy().T.reshape(-1).view(np.uint16),
+                                  g["x_scale"].reshape(-1).view(np.uint16))
+    y = y.cpu().numpy().astype(np.float64)
+    y_exact, absdot, bound = linear_bound(x16, w16, g["x_scale"].reshape(-1), g["w_scale"].reshape(-1), abits)
+    gy = g["y"].astype(np.float64)
+    # the reference's own F.linear (fp16, CPU) sits within its fp16 noise of the exact product ...
+    assert np.all(np.abs(gy - y_exact) <= 1e-3 * absdot)
+    # ... the HIP output within the code-difference bound (+ fp16 output rounding) of it ...
+    assert np.all(np.abs(y - y_exact) <= bound + 2e-4 * absdot + 1e-3 * np.abs(y_exact))
+    # ... and therefore of the reference's own numbers
+    err = np.abs(y - gy)
+    assert np.all(err <= bound + 1.2e-3 * absdot + 1e-3 * np.abs(y_exact)), float((err - bound).max())

@@ -297,39 +297,67 @@ def test_linear_edge_inputs(ops, dev):
             assert_gemm_close(host(d), ref, mag, f"linear edge {name} a{abits}")
 
 
-def test_bmma_state_api_reference_layout(ops, dev):
-    """FQBMMAInitFn/ExecFn-style call on reference bit-plane X (flexq_bmma_op.h:163-188)."""
+@pytest.mark.parametrize("M,N,K,abits", [(4, 256, 1024, 6), (1, 512, 8192, 8), (16, 200, 512, 6)])
+def test_bmma_state_api_reference_layout(ops, dev, M, N, K, abits):
+    """FQBMMAInitFn/ExecFn-style calls (flexq_bmma_op.h:163-188) on the reference's own operands:
+    bit-plane X and W plus X_SCALE (duplicated layout) and W_SCALE, into UNinitialised scratch
+    (torch.empty; the first exec zeroes its ticket region and imports W).  (1, 512, 8192) plans a
+    split-K decode (S > 1), so garbage tickets would show; N = 200 is ragged (bit-plane rows 8k).
+    The image fast path (fq_bmma_init_image) gives the same bits, and repeated execs are stable."""
     import ctypes
     from flexq_amd import _lib
-    M, N, K, abits = 4, 256, 1024, 6
-    xraw, wraw, xq, wq, xs, ws = kat_operands(M, N, K, abits, seed=77)
+    L = _lib.load()
+    if M == 1:
+        assert L.fq_gemm_workspace_bytes(M, N, K) > 0  # the split-K plan
+    xraw, wraw, xq, wq, xs, ws = kat_operands(M, N, K, abits, seed=77 + M)
     X = to_dev(oracle.pack_bitplanes(xraw, abits), dev)
-    W = ops.import_ref_w(to_dev(oracle.pack_bitplanes(wraw, 6), dev), to_dev(ws, dev), N, K)
+    W = to_dev(oracle.pack_bitplanes(wraw, 6), dev)
     XS = to_dev(oracle.xs_to_ref_dup(xs, M, K), dev)
     WS = to_dev(ws, dev)
-    D = torch.empty((M, N), dtype=torch.float16, device=dev)
-    L = _lib.load()
-    nb = L.fq_bmma_scratch_bytes(M, N, K)
-    scratch = torch.zeros(max(nb, 1), dtype=torch.uint8, device=dev)
-
-    class State(ctypes.Structure):
-        _fields_ = [("init_success", ctypes.c_int), ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
-                    ("x_bits", ctypes.c_int), ("w_bits", ctypes.c_int), ("group_size", ctypes.c_int),
-                    ("X", ctypes.c_void_p), ("W", ctypes.c_void_p), ("X_SCALE", ctypes.c_void_p),
-                    ("W_SCALE", ctypes.c_void_p), ("D", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
-                    ("scratch_bytes", ctypes.c_size_t)]
-    L.fq_bmma_init.restype = State
-    L.fq_bmma_init.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_size_t]
-    L.fq_bmma_exec.argtypes = [ctypes.POINTER(State), ctypes.c_void_p]
-    st = L.fq_bmma_init(X.data_ptr(), W.data_ptr(), XS.data_ptr(), WS.data_ptr(), M, N, K, D.data_ptr(), 128, 0,
-                        abits, 6, scratch.data_ptr(), scratch.numel())
-    assert st.init_success == 1
-    bad = L.fq_bmma_init(X.data_ptr(), W.data_ptr(), XS.data_ptr(), WS.data_ptr(), M, N, K, D.data_ptr(), 64, 0,
-                         abits, 6, scratch.data_ptr(), scratch.numel())
-    assert bad.init_success == 0  # group_size != 128 is rejected like FQBMMAOp::initialize
-    assert L.fq_bmma_exec(ctypes.byref(st), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ref, _, mag = oracle.gemm(xq, xs, wq, ws)
-    assert_gemm_close(host(D), ref, mag, "bmma state api")
+    outs = []
+    for image in (False, True):
+        D = torch.full((M, N), float("nan"), dtype=torch.float16, device=dev)
+        nb = (L.fq_bmma_image_scratch_bytes if image else L.fq_bmma_scratch_bytes)(M, N, K)
+        scratch = torch.empty(nb, dtype=torch.uint8, device=dev)
+        scratch.fill_(0xA5)  # garbage everywhere, tickets included
+        if image:
+            img = ops.import_ref_w(W, WS, N, K)
+            st = L.fq_bmma_init_image(X.data_ptr(), img.data_ptr(), XS.data_ptr(), M, N, K, D.data_ptr(), 128, 0,
+                                      abits, 6, scratch.data_ptr(), nb)
+        else:
+            st = L.fq_bmma_init(X.data_ptr(), W.data_ptr(), XS.data_ptr(), WS.data_ptr(), M, N, K, D.data_ptr(),
+                                128, 0, abits, 6, scratch.data_ptr(), nb)
+        assert st.init_success == 1 and st.prepared == 0
+        for _ in range(3):
+            assert L.fq_bmma_exec(ctypes.byref(st), stream) == 0
+            assert st.prepared == 1
+            assert_gemm_close(host(D), ref, mag, f"bmma state api image={image}")
+            outs.append(host(D).view(np.uint16).copy())
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+
+
+def test_bmma_init_rejections(ops, dev):
+    """The rejections of FQBMMAOp::initialize (flexq_bmma_op.h:103-126) as init_success = 0."""
+    from flexq_amd import _lib
+    L = _lib.load()
+    M, N, K = 4, 256, 1024
+    nb = L.fq_bmma_scratch_bytes(M, N, K)
+    buf = torch.empty(nb, dtype=torch.uint8, device=dev)
+    p = buf.data_ptr()
+
+    def init(**kw):
+        a = dict(X=p, W=p, XS=p, WS=p, M=M, N=N, K=K, D=p, g=128, bias=0, xb=6, wb=6, s=p, nb=nb)
+        a.update(kw)
+        return L.fq_bmma_init(a["X"], a["W"], a["XS"], a["WS"], a["M"], a["N"], a["K"], a["D"], a["g"], a["bias"],
+                              a["xb"], a["wb"], a["s"], a["nb"]).init_success
+    assert init() == 1
+    for kw in (dict(g=64), dict(bias=1), dict(K=1000), dict(xb=4), dict(wb=8), dict(WS=None), dict(W=None),
+               dict(M=12), dict(N=20), dict(nb=nb - 1), dict(s=None)):
+        assert init(**kw) == 0, kw
+    assert L.fq_bmma_image_scratch_bytes(M, N, K) < nb  # no image region on the fast path
 
 
 def test_split_k_after_prefill_on_shared_workspace(ops, dev):
@@ -358,6 +386,44 @@ def test_split_k_after_prefill_on_shared_workspace(ops, dev):
         assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
     ref, _, mag = oracle.gemm(host(xq), host(xs), host(wq), host(ws))
     assert_gemm_close(host(d1), ref, mag, "split-K after prefill")
+
+
+def test_workspace_growth_keeps_captured_graphs_valid(ops, dev):
+    """A graph captured with the stream's workspace bakes its address (split-K tickets + slabs)
+    into the launch.  Growing the workspace afterwards (a prefill on the same stream) must not free
+    it: the replay stays exact even after the allocator hands out and scribbles over new memory."""
+    from flexq_amd import _lib
+    L = _lib.load()
+    M, N, K = 1, 512, 8192  # split-K decode (tickets + slabs in the workspace)
+    assert 0 < L.fq_gemm_workspace_bytes(M, N, K) < L.fq_gemm_workspace_bytes(2048, 2048, 4096)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+    pk = ops.pack_w6(torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g),
+                     (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half())
+    s = torch.cuda.Stream(dev)  # a fresh stream: its workspace is created by the first call
+    out = torch.empty((M, N), dtype=torch.float16, device=dev)
+    with torch.cuda.stream(s):
+        ops.linear_w6ax(x, pk, N, 6, out=out)
+    torch.cuda.synchronize()
+    want = out.clone()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        ops.linear_w6ax(x, pk, N, 6, out=out)
+    # grow the stream's workspace: the prefill U8 path wants the unpack buffer
+    xp = torch.randint(-128, 128, (2048, 4096), dtype=torch.int8, device=dev, generator=g)
+    xsp = (torch.rand((32, 2048), device=dev, generator=g) * 0.05).half()
+    pkp = ops.pack_w6(torch.randint(-32, 32, (2048, 4096), dtype=torch.int8, device=dev, generator=g),
+                      (torch.rand((32, 2048), device=dev, generator=g) * 0.05).half())
+    with torch.cuda.stream(s):
+        ops.gemm_w6ax(xp, xsp, pkp, 2048, 8)
+    torch.cuda.synchronize()
+    junk = [torch.full((1 << 20,), -1, dtype=torch.int32, device=dev) for _ in range(8)]  # reuse freed blocks
+    for _ in range(3):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int16), want.view(torch.int16))
+    del junk
 
 
 @pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (4096, 4096, 4096)])

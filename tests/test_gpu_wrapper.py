@@ -1,0 +1,40 @@
+"""The in-tree C++ FLEXQGEMMWrapper drop-in (include/flexq_gemm_wrapper.hpp; the reference's
+flexq_gemm_wrapper.h:6-48) driven from a compiled C++ program (tests/cpp/test_wrapper.cpp, built by
+__graft_entry__.build()) exactly as a FasterTransformer layer calls it: bit-plane weights + W_SCALE,
+gemm(const half* A ...) and pack() + gemm(const int* A ...).  Its outputs are checked here against
+the CPU oracle on the inputs it wrote."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from common import ROOT, assert_gemm_close, oracle
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "tests", "cpp", "test_wrapper")
+
+
+@pytest.mark.parametrize("M,N,K,abits", [(1, 512, 8192, 6), (4, 256, 1024, 8), (16, 4096, 4096, 8),
+                                         (64, 384, 512, 6), (8, 200, 2048, 6)])
+def test_cpp_wrapper_against_oracle(dev, tmp_path, M, N, K, abits):
+    assert os.path.exists(BIN), "build first: __graft_entry__.build() compiles tests/cpp/test_wrapper"
+    r = subprocess.run([BIN, str(tmp_path), str(M), str(N), str(K), str(abits), str(M * N + K)],
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "[FlexQ][Error]" in r.stderr  # the deliberate rejections print like the reference
+
+    def load(name, dt, shape):
+        return np.fromfile(os.path.join(tmp_path, name), dtype=dt).reshape(shape)
+    x = load("x.f16", np.float16, (M, K))
+    wraw = load("wraw.i32", np.int32, (N, K))
+    ws = load("ws.f16", np.float16, (K // 128, N))
+    d_half = load("d_half.f16", np.float16, (M, N))
+    d_int = load("d_int.f16", np.float16, (M, N))
+    xq, xs = oracle.quantize_engine(x, abits)
+    wq = ((wraw ^ 32) - 32).astype(np.int8)
+    ref, _, mag = oracle.gemm(xq, xs, wq, ws)
+    assert_gemm_close(d_half, ref, mag, "wrapper gemm(const half*)")
+    # pack() + gemm(const int*) quantizes with the same rule and runs the same GEMM
+    np.testing.assert_array_equal(d_int.view(np.uint16), d_half.view(np.uint16))
