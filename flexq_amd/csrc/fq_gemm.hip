@@ -40,6 +40,10 @@
 //     no float atomics.  (MI355X_MICROARCH.md "Valid forms", row 1.)
 // =============================================================================================
 
+// cache policy of the weight stream's LDS-DMA (aux: 2 = nt, once-read bytes)
+#ifndef FQ_W_AUX
+#define FQ_W_AUX 2
+#endif
 // waves per WG (one WG per CU): 8, or 4 for 32-row tiles (their reduction buffers are larger)
 #ifndef FQ_DECODE_WAVES
 #define FQ_DECODE_WAVES 8
@@ -234,8 +238,8 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
         const int t = item_tile(it), g = ga + j;
         char *dst = ring + slot * C::SLOT;
         const char *src = wbytes + ((long)t * G + g) * FQ_BLOCK;
-        __builtin_amdgcn_global_load_lds(src, LDS_PTR(dst), 16, 0, 2 /*nt*/);
-        if (lane < 32) __builtin_amdgcn_global_load_lds(src + 1024, LDS_PTR(dst + 1024), 16, 0, 2);
+        __builtin_amdgcn_global_load_lds(src, LDS_PTR(dst), 16, 0, FQ_W_AUX);
+        if (lane < 32) __builtin_amdgcn_global_load_lds(src + 1024, LDS_PTR(dst + 1024), 16, 0, FQ_W_AUX);
 #pragma unroll
         for (int p = 0; p < C::XP; p++) {  // activation rows [MT][128 B], swizzled chunks
             const int row = p * 8 + (lane >> 3), chunk = (lane & 7) ^ (row & 7);

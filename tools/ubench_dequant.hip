@@ -1,0 +1,157 @@
+// ubench_dequant.hip -- development microbenchmark: the prefill inner block (int8 MFMA + the
+// per-group dequant of the reference's epilogue: cvt_f32_i32 + fma_mix with the fp16 scale
+// product) on registers only, to find the issue ceiling of each formulation (cycles per MFMA per
+// SIMD) at 1 and 2 waves per SIMD.  Not part of the product.
+// build: hipcc -O3 --offload-arch=gfx950 -fno-slp-vectorize tools/ubench_dequant.hip -o /tmp/ubd
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+template <int MODE, int W>  // 0: MFMA only, 1: 16x16x64 + dequant, 2: 32x32x32 + dequant
+__global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float *sink) {
+    extern __shared__ char lds[];  // sized by the launch to force one block per CU
+    const int lane = threadIdx.x & 63;
+    v4i a[4][2], b[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            a[i][s] = v4i{lane * 3 + i, lane + s, lane ^ i, 7 * lane};
+            b[i][s] = v4i{lane ^ 9, lane * 5 + s, i + lane, lane};
+        }
+    uint32_t xv[4], wv[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        xv[i] = 0x3c003c00u + lane + i;
+        wv[i][0] = 0x2c002c00u + lane * i;
+        wv[i][1] = 0x2c012c01u + lane * i;
+    }
+    float out[4][4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) out[i][j][r] = 0.f;
+    v16i acc32[2][2];
+    float (*out32)[2][16] = reinterpret_cast<float (*)[2][16]>(&out[0][0][0]);  // the same 64 registers
+    long long t0 = clock64();
+    for (int it = 0; it < iters; it++) {
+        asm volatile("" : "+v"(a[0][0]), "+v"(b[0][0]), "+v"(xv[0]), "+v"(wv[0][0]));
+        if (MODE == 0) {
+#pragma unroll
+            for (int mi = 0; mi < 4; mi++)
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++) {
+                    v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
+                    out[mi][ni][0] += __int_as_float(acc[0] ^ acc[3]);
+                }
+        } else if (MODE == 1) {
+#pragma unroll
+            for (int mi = 0; mi < 4; mi++) {
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++) {
+                    v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
+                    const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+                    const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                    const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                    float *o = out[mi][ni];
+                    o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
+                    o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
+                    o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
+                    o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
+                }
+            }
+        } else {
+            // 32x32x32: a wave tile of 64x64 = 2x2 blocks; k = 128 = 4 MFMAs per block
+#pragma unroll
+            for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++) {
+                    v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni][0], a[2 * mi][0], v16i{}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni][1], a[2 * mi][1], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni + 1][0], a[2 * mi + 1][0], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni + 1][1], a[2 * mi + 1][1], acc, 0, 0, 0);
+                    acc32[mi][ni] = acc;
+                }
+#pragma unroll
+            for (int mi = 0; mi < 2; mi++) {
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t w01 = wv[2 * ni + (q >> 1)][q & 1], w23 = wv[2 * ni + (q >> 1)][(q & 1) ^ 1];
+                        const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                        const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                        float *o = &out32[mi][ni][4 * q];
+                        o[0] = fmaf((float)acc32[mi][ni][4 * q + 0], __low2float(p01), o[0]);
+                        o[1] = fmaf((float)acc32[mi][ni][4 * q + 1], __high2float(p01), o[1]);
+                        o[2] = fmaf((float)acc32[mi][ni][4 * q + 2], __low2float(p23), o[2]);
+                        o[3] = fmaf((float)acc32[mi][ni][4 * q + 3], __high2float(p23), o[3]);
+                    }
+            }
+        }
+    }
+    long long t1 = clock64();
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) s += out[i][j][r];
+    if (s == 1234.5f) sink[blockIdx.x] = s + lds[0];
+    if (threadIdx.x == 0 && blockIdx.x == 0) *cyc = t1 - t0;
+}
+
+template <int MODE, int waves>
+static void run(const char *name) {
+    long long *cyc;
+    float *sink;
+    hipMalloc(&cyc, 8);
+    hipMalloc(&sink, 4096 * 4);
+    const int iters = 2000;
+    hipFuncSetAttribute((const void *)kern<MODE, waves>, hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int rep = 0; rep < 2; rep++) {
+        hipEventRecord(e0);
+        hipLaunchKernelGGL((kern<MODE, waves>), dim3(256), dim3(64 * waves), 100 * 1024, 0, iters, cyc, sink);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+    }
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    long long c;
+    hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+    const int mfma_per_iter = MODE == 2 ? 16 : 32;            // per wave
+    const double macs = (double)256 * waves * iters * 16 * 16 * 128 * 16;  // 16 blocks of 16x16x128 (or 4 of 32x32x128)
+    const double wps = waves / 4.0;                            // waves per SIMD
+    printf("%-28s waves/SIMD=%.0f  cycles/iter/wave=%7.1f  SIMD cycles per 16x16x128 block=%6.1f (ideal 32)  TOPS=%7.1f\n",
+           name, wps, (double)c / iters, (double)c / iters / (16 * wps), 2 * macs / (ms * 1e-3) / 1e12);
+    (void)mfma_per_iter;
+}
+
+int main() {
+    run<0, 4>("mfma only 16x16x64");
+    run<1, 4>("16x16x64 + dequant");
+    run<2, 4>("32x32x32 + dequant");
+    run<0, 8>("mfma only 16x16x64");
+    run<1, 8>("16x16x64 + dequant");
+    run<2, 8>("32x32x32 + dequant");
+    run<1, 12>("16x16x64 + dequant");
+    run<2, 12>("32x32x32 + dequant");
+    return 0;
+}
