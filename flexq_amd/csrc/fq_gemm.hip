@@ -1001,12 +1001,22 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
 #ifdef FQ_DEV_ABLATION
     if (!acc_dbg && dev_ablation() >= 1 && dev_ablation() <= 127) {
         const int abl = dev_ablation();
+        const bool u8 = M >= PF_U8_MIN_M && workspace && workspace_bytes >= kTicketBytes + prefill_u8_bytes(N, K);
+        char *wu = u8 ? (char *)workspace + kTicketBytes : nullptr;
+        if (u8) {
+            const long nblk = (long)NT * (K / FQ_GROUP);
+            hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0, s,
+                               (const char *)w_packed, nblk, wu);
+        }
 #define FQ_PABL(v)                                                                                         \
-        if (abl == v)                                                                                        \
+        if (abl == v && u8)                                                                                  \
+            hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, v, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, \
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);        \
+        if (abl == v && !u8)                                                                                 \
             hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, v>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs, \
                                (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
         FQ_PABL(1) FQ_PABL(2) FQ_PABL(3) FQ_PABL(4) FQ_PABL(5) FQ_PABL(7) FQ_PABL(8) FQ_PABL(11) FQ_PABL(15)
-        FQ_PABL(16) FQ_PABL(31) FQ_PABL(35) FQ_PABL(67) FQ_PABL(99)
+        FQ_PABL(16) FQ_PABL(31) FQ_PABL(35) FQ_PABL(67) FQ_PABL(99) FQ_PABL(6) FQ_PABL(12) FQ_PABL(17) FQ_PABL(19)
 #undef FQ_PABL
         FQ_LAUNCH_CHECK();
         return FQ_OK;

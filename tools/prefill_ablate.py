@@ -1,6 +1,7 @@
 """Prefill GEMM ablations (development tool; needs tools/libflexq_hip_abl.so, `make -C
 flexq_amd/csrc abl`).  FQ_DEV_ABLATION bits: 1 no dequant, 2 no MFMA, 4 no LDS reads,
-8 no global loads / DMA.
+8 no global loads / DMA, 16 no stores, 32 no A DMA, 64 no weight loads.  M >= 2048: the U8 path
+(weights unpacked once per call) like the product.
 usage: python tools/prefill_ablate.py M N K"""
 import os
 import sys
@@ -25,7 +26,7 @@ def main():
     xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
     xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.01).half()
     out = torch.empty((M, N), device=dev, dtype=torch.float16)
-    for m in (0, 3, 35, 67, 99):
+    for m in [int(v) for v in os.environ.get("FQ_ABL_LIST", "0,1,2,3,4,5,6,7,8,12,16,17,19").split(",")]:
         os.environ["FQ_DEV_ABLATION"] = str(m)
         for _ in range(3):
             ops.gemm_w6ax(xq, xs, img, N, 8, out=out)
