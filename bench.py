@@ -437,6 +437,85 @@ def measure_tp(ctx, cfg, merge, tp, steps, warmup):
                 launches_per_step=n_lin, fused_launches=all(fused.values()), graph=use_graph, finite=finite)
 
 
+def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
+    """SURVEY.md §8(f)3 / README.md:193: LLaMA-2-7B decoder layers end to end (norms, SiLU*up,
+    the four linears, residuals; the attention core is out of scope and stands in as ctx = v,
+    exact attention over a single position) in FT's tensor-parallel layout over the ranks --
+    qkv and gate_up column-parallel, o_proj and down_proj row-parallel + one all-reduce each
+    (flexq_amd.layers.FlexQDecoderLayer) -- against the same layers in fp16 torch ops (F.rms_norm,
+    hipBLASLt F.linear, F.silu, the same all-reduces), both as one HIP graph over `layers` layers.
+    Returns ms per token step for both and, with several ranks, the W6 step without its
+    all-reduces."""
+    from flexq_amd import convert
+    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear
+    dev, tp, rank = ctx.dev, ctx.world, ctx.rank
+    g = torch.Generator(device=dev).manual_seed(seed)  # the same full weights on every rank
+    sq, sf = H ** -0.5, F ** -0.5
+    w6, w16 = [], []
+    for _ in range(layers):
+        q, k, v, o = (torch.randn((H, H), device=dev, generator=g) * sq for _ in range(4))
+        gate, up = (torch.randn((F, H), device=dev, generator=g) * sq for _ in range(2))
+        down = torch.randn((H, F), device=dev, generator=g) * sf
+        qkv_p = convert.shard_parts([q.half(), k.half(), v.half()], tp, rank)
+        o_p, _ = convert.shard_columns(o.half(), tp, rank)
+        gu_p = convert.shard_parts([gate.half(), up.half()], tp, rank, by_group=True)
+        down_p, _ = convert.shard_columns(down.half(), tp, rank)
+        del q, k, v, o, gate, up, down
+        ga = torch.ones(H, dtype=torch.float16, device=dev)
+        lin = lambda w, ab, row: W6Linear(ops.quantize_pack_w6(w)[0], w.shape[0], w.shape[1], ab,  # noqa: E731
+                                          row_parallel=row and tp > 1)
+        w6.append(FlexQDecoderLayer(lin(qkv_p, 6, False), lin(o_p, 6, True),
+                                    FlexQFfn(lin(gu_p, 6, False), lin(down_p, 8, True), ga), ga,
+                                    lambda qkv: qkv[:, 2 * qkv.shape[1] // 3:]))
+        w16.append(dict(qkv=qkv_p, o=o_p, gu=gu_p, down=down_p, ga=ga, Fp=down_p.shape[1]))
+    torch.cuda.synchronize()
+
+    def allreduce(t):
+        if tp > 1 and not ctx.staged:
+            dist.all_reduce(t)
+
+    def step_w6(h, reduce=True):
+        for L in w6:
+            a = L.attention(h, reduce=reduce)
+            y = L.ffn(h, a, reduce=reduce)
+            h += y
+
+    def step_16(h):
+        F_ = torch.nn.functional
+        for W in w16:
+            x = F_.rms_norm(h, (H,), W["ga"], 1e-6)
+            qkv = F_.linear(x, W["qkv"])
+            a = F_.linear(qkv[:, 2 * qkv.shape[1] // 3:], W["o"])
+            allreduce(a)
+            h += a
+            x = F_.rms_norm(h, (H,), W["ga"], 1e-6)
+            gu = F_.linear(x, W["gu"])
+            y = F_.linear(F_.silu(gu[:, :W["Fp"]]) * gu[:, W["Fp"]:], W["down"])
+            allreduce(y)
+            h += y
+
+    out = {}
+    h0 = torch.randn((M, H), dtype=torch.float16, device=dev, generator=g)
+    hs = {k: h0.clone() for k in ("w6", "w6_noreduce", "fp16")}
+    fns = {"w6": lambda: step_w6(hs["w6"]), "fp16": lambda: step_16(hs["fp16"])}
+    if tp > 1:
+        fns["w6_noreduce"] = lambda: step_w6(hs["w6_noreduce"], reduce=False)
+    for name, fn in fns.items():
+        replay = ctx.prepare(fn, not ctx.a.no_graph and not ctx.staged)
+        el, _ = ctx.timed(replay, reps, 2)
+        out[name] = el / reps * 1e3
+        hs[name].copy_(h0)
+    res = {"w6_ms_per_step": round(out["w6"], 4), "fp16_ms_per_step": round(out["fp16"], 4),
+           "speedup_vs_fp16": round(out["fp16"] / out["w6"], 3), "tok_per_s": round(M * 1e3 / out["w6"], 2),
+           "fp16_tok_per_s": round(M * 1e3 / out["fp16"], 2)}
+    if tp > 1:
+        res["w6_no_allreduce_ms_per_step"] = round(out["w6_noreduce"], 4)
+        res["allreduce_share"] = round(max(0.0, 1 - out["w6_noreduce"] / out["w6"]), 4)
+    del w6, w16
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -458,6 +537,8 @@ def main():
     ap.add_argument("--no-replicas", action="store_true", help="N > 1, tp: skip the replica (dp) measurement")
     ap.add_argument("--no-c4", action="store_true",
                     help="N > 1: skip the LLaMA-2-70B column-parallel measurement (BASELINE config C4)")
+    ap.add_argument("--no-layers", action="store_true",
+                    help="skip the end-to-end decoder-layer comparison against fp16 (M = 1 and 16)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo with host-staged gathers, no graph")
     a = ap.parse_args()
@@ -627,6 +708,14 @@ def main():
                 **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in rc.items()
                    if k not in ("elapsed", "flops_step")},
                 "hbm_frac_per_rank": round(rc["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
+    if not a.no_layers and not prefill and a.config.startswith("llama2-7b"):
+        res["decoder_layers_e2e"] = {
+            "what": f"LLaMA-2-7B decoder layers end to end (32 layers; RMSNorm, qkv, o, gate_up, SiLU*up, down, "
+                    f"residuals; attention core out of scope: ctx = v), FT's TP layout over {world} rank(s) "
+                    f"(row-parallel o/down + one all-reduce each), W6A6 (down W6A8) engine vs fp16 torch "
+                    f"(F.rms_norm, hipBLASLt F.linear, F.silu), one HIP graph each; README.md:193's comparison",
+            "tp": world,
+            **{f"M{m}": decoder_layers_e2e(ctx, m) for m in (1, 16)}}
     if world == 1 and not a.no_calibrate:
         res["roofline"]["peak_measured"] = calibrate_peaks(dev)
         pm = res["roofline"]["peak_measured"]
