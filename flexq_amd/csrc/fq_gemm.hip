@@ -746,6 +746,191 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     }
 }
 
+// Large-M prefill on 256 x 256 workgroup tiles (the U8 path, M >= PF_U8_MIN_M).  Measured on the
+// 128 x 128 kernel above (tools/prefill_ablate.py, M = 16384): its data-movement skeleton alone --
+// no MFMA, no dequant -- takes 47 % of the launch, and per CU and group step it moves 72 LDS-DMA
+// pieces (TA-issued at ~30 cycles each) and reads 128 KiB of fragments from LDS (1024 cycles at
+// 128 B/clk) for 4.2 M MACs (1031 MFMA cycles at peak): the LDS and the address unit, not the
+// MFMA, bound it.  Here one workgroup of 8 waves per CU owns 256 rows x 256 columns; each wave a
+// 128 x 64 tile (8 x 4 blocks of 16 x 16, the same MFMA core, dequant, operand layouts and
+// epilogue as fq_gemm_prefill_kernel): per group step 66 DMA pieces and 192 KiB of fragment
+// reads for 8.4 M MACs -- half the DMA and three quarters of the LDS reads per MAC.  Two stages
+// of 65.5 KiB (A 32 KiB + scales, unpacked B 32 KiB).  Bit-identical to the 128 x 128 kernels.
+constexpr int PB_BM = 256, PB_TILES = 16, PB_WAVES = 8;
+constexpr int PB_XS_OFF = PB_BM * FQ_GROUP;          // A: 32 KiB, then the x-scales, one per dword
+constexpr int PB_WS_OFF = PB_XS_OFF + PB_BM * 4;     // w-scales of the 16 tiles (fp16 [16][16])
+constexpr int PB_ASTAGE = PB_WS_OFF + PB_TILES * 32; // 33.5 KiB
+constexpr int PB_BSTAGE = PB_TILES * 2 * 1024;       // unpacked B: [tile][k-step][lane][16 B]
+
+template <bool DBG>
+__global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
+    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
+    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu) {
+    extern __shared__ __attribute__((aligned(16))) char pb_smem[];
+    char *sa = pb_smem, *sbu = pb_smem + 2 * PB_ASTAGE;
+    const int G = K / FQ_GROUP, NT = (N + 15) / 16;
+    const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid >> 2, wn = wid & 3;  // 2 x 4 waves of 128 rows x 64 columns
+
+    // Block order as in fq_gemm_prefill_kernel: XCD remap, then groups of 8 M-panels
+    const int nbm = (M + PB_BM - 1) / PB_BM, nbn = (NT + PB_TILES - 1) / PB_TILES, nwg = nbm * nbn;
+    const int bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+    const int span = 8 * nbn, first = (lid / span) * 8;
+    const int gsz = nbm - first < 8 ? nbm - first : 8;
+    const int bm = first + (lid % span) % gsz, bn = (lid % span) / gsz;
+    const int m0 = bm * PB_BM, t0 = bn * PB_TILES;
+
+    // per-lane DMA sources at group 0: wave w stages A rows 32 w .. 32 w + 31 (4 pieces), the
+    // unpacked B of tiles 2 w, 2 w + 1 (4 pieces); waves 0-3 the x-scales of 64 rows each, wave 4
+    // the w-scales of the 16 tiles
+    const int8_t *asrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int row = 32 * wid + 8 * i + (lane >> 3);
+        const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M are computed, never stored
+        asrc[i] = xq + (size_t)m * K + ((lane & 7) ^ (row & 7)) * 16;
+    }
+    const int srow = 64 * (wid & 3) + lane;
+    const uint16_t *xsrc = xs + (m0 + srow < M ? m0 + srow : M - 1);
+    const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;
+    const uint16_t *wsrc = wsb + (size_t)wt * G * 16 + 8 * (lane & 1);
+    const char *usrc[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const int ut = t0 + 2 * wid + t < NT ? t0 + 2 * wid + t : NT - 1;
+        usrc[t] = wu + (size_t)ut * G * 2048 + lane * 16;
+    }
+    auto stage = [&](int g, int slot) {
+        char *buf = sa + slot * PB_ASTAGE;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            __builtin_amdgcn_global_load_lds(asrc[i] + g * FQ_GROUP, LDS_PTR(buf + (32 * wid + 8 * i) * FQ_GROUP), 16, 0, 0);
+        if (wid < 4)
+            __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PB_XS_OFF + 64 * wid * 4), 2, 0, 0);
+        else if (wid == 4 && lane < 32)
+            __builtin_amdgcn_global_load_lds(wsrc + g * 16, LDS_PTR(buf + PB_WS_OFF), 16, 0, 0);
+        char *bdst = sbu + slot * PB_BSTAGE + 2 * wid * 2048;
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+                __builtin_amdgcn_global_load_lds(usrc[t] + (size_t)g * 2048 + k * 1024, LDS_PTR(bdst + t * 2048 + k * 1024), 16, 0, 0);
+    };
+
+    const uint32_t la = lds_addr(sa), lbu = lds_addr(sbu);
+    const int arow = wm * 128 + (lane & 15);
+    const uint32_t a_off0 = arow * FQ_GROUP + xswz(arow, lane >> 4), a_off1 = arow * FQ_GROUP + xswz(arow, 4 + (lane >> 4));
+    const uint32_t x_off = PB_XS_OFF + arow * 4;
+    const uint32_t w_off = PB_WS_OFF + (wn * 64 + 4 * (lane >> 4)) * 2;
+    const uint32_t b_off = wn * 4 * 2048 + lane * 16;
+
+    float out[8][4][4];  // [mi][ni][r]: row 16 mi + (lane & 15), column 16 ni + 4 (lane >> 4) + r
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) out[i][j][r] = 0.f;
+
+    stage(0, 0);
+    __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
+    for (int g = 0; g < G; g++) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        stage(g + 1 < G ? g + 1 : G - 1, (g + 1) & 1);  // (past the last group: a never-read copy)
+        const uint32_t ab = la + (g & 1) * PB_ASTAGE, bb = lbu + (g & 1) * PB_BSTAGE + b_off;
+        v4i b[4][2];
+        v2u wv[4];
+        v4i a[3][2];  // row blocks mi, mi + 1 and mi + 2 in flight
+        uint32_t xv[3];
+#define FQ_PB_B(ni)                                                \
+        b[ni][0] = ds_read_b128_at<(ni) * 2048>(bb);                \
+        b[ni][1] = ds_read_b128_at<(ni) * 2048 + 1024>(bb);         \
+        wv[ni] = ds_read_b64_at<(ni) * 32>(ab + w_off);
+        FQ_PB_B(0) FQ_PB_B(1) FQ_PB_B(2) FQ_PB_B(3)
+#undef FQ_PB_B
+#define FQ_PB_A(mi)                                                                  \
+        a[(mi) % 3][0] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off0);          \
+        a[(mi) % 3][1] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off1);          \
+        xv[(mi) % 3] = ds_read_b32_at<(mi) * 64>(ab + x_off);
+        FQ_PB_A(0) FQ_PB_A(1)
+        // in flight: B (8) + w-scales (4) + rows 0, 1 (3 each); each row block's reads are waited
+        // for with the next-but-one block's (3) and the next one's (3) still outstanding
+        asm volatile("s_waitcnt lgkmcnt(3)"
+                     : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]),
+                       "+v"(b[3][0]), "+v"(b[3][1]), "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]),
+                       "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
+#pragma unroll
+        for (int mi = 0; mi < 8; mi++) {
+            const int c = mi % 3;
+            if (mi > 0) {  // row block mi landed; mi + 1 may still be in flight
+                if (mi + 1 < 8)
+                    asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+                else
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+            }
+            // issue row block mi + 2 into the slot row block mi - 1 used (its MFMAs are issued)
+            if (mi + 2 < 8) {
+                const int c2 = (mi + 2) % 3;
+                const uint32_t ro = (mi + 2) * 16 * FQ_GROUP;
+                a[c2][0] = ds_read_b128(ab + a_off0 + ro);
+                a[c2][1] = ds_read_b128(ab + a_off1 + ro);
+                xv[c2] = ds_read_b32_at<0>(ab + x_off + (mi + 2) * 64);
+            }
+            const uint32_t x2u = __builtin_amdgcn_perm(xv[c], xv[c], 0x01000100u);  // half2(xs, xs)
+            const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++) {
+                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[c][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[c][1], acc, 0, 0, 0);
+                const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);  // fp16-rounded
+                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);  // scale product
+                float *o = out[mi][ni];
+                o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
+                o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
+                o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
+                o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
+                if (DBG) {
+                    const int m = m0 + arow + mi * 16;
+                    const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        if (m < M && n + r < N) acc_dbg[((size_t)m * N + n + r) * G + g] = acc[r] >> 2;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(vmcnt_only(0));  // stage g + 1 landed
+    }
+
+    const bool vec = (N & 3) == 0;
+#pragma unroll
+    for (int mi = 0; mi < 8; mi++) {
+        const int m = m0 + arow + mi * 16;
+        if (m >= M) continue;
+#pragma unroll
+        for (int ni = 0; ni < 4; ni++) {
+            const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
+            const float *o = out[mi][ni];
+            uint16_t *dst = d + (size_t)m * N + n;
+            if (vec && n + 3 < N) {
+                const uint32_t lo = (uint32_t)f2h(o[0] * 0.25f) | ((uint32_t)f2h(o[1] * 0.25f) << 16);
+                const uint32_t hi = (uint32_t)f2h(o[2] * 0.25f) | ((uint32_t)f2h(o[3] * 0.25f) << 16);
+                *reinterpret_cast<uint2 *>(dst) = make_uint2(lo, hi);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    if (n + r < N) dst[r] = f2h(o[r] * 0.25f);
+            }
+        }
+    }
+}
+
 // =============================================================================================
 // Host side: plan + launch
 // =============================================================================================
@@ -1031,11 +1216,13 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         char *wu = (char *)workspace + kTicketBytes;
         hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0, s,
                            (const char *)w_packed, nblk, wu);
+        const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
+        const size_t lds_big = 2 * (size_t)(PB_ASTAGE + PB_BSTAGE);
         if (acc_dbg)
-            hipLaunchKernelGGL((fq_gemm_prefill_kernel<true, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+            hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<true>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s,
                                xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
         else
-            hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+            hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<false>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s,
                                xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
         FQ_LAUNCH_CHECK();
         return FQ_OK;

@@ -8,12 +8,15 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from flexq_amd import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.environ.get("FQ_LIB", _lib.LIB_PATH)  # development variants (tools/libflexq_*.so)
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
 
 
-def timed(fn, reps=10):
+def timed(fn, reps=int(os.environ.get("FQ_REPS", "10"))):
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
