@@ -71,6 +71,30 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
                     o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
                 }
             }
+        } else if (MODE == 3 || MODE == 4 || MODE == 5) {  // 3: no pk_mul, 4: no cvt, 5: neither
+#pragma unroll
+            for (int mi = 0; mi < 4; mi++) {
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++) {
+                    v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
+                    uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+                    __half2 p01 = *reinterpret_cast<const __half2 *>(&w01), p23 = *reinterpret_cast<const __half2 *>(&w23);
+                    if (MODE == 4) {
+                        p01 = __hmul2(p01, x2);
+                        p23 = __hmul2(p23, x2);
+                    }
+                    float *o = out[mi][ni];
+#define CV(v) (MODE == 3 ? (float)(v) : __int_as_float(v))
+                    o[0] = fmaf(CV(acc[0]), __low2float(p01), o[0]);
+                    o[1] = fmaf(CV(acc[1]), __high2float(p01), o[1]);
+                    o[2] = fmaf(CV(acc[2]), __low2float(p23), o[2]);
+                    o[3] = fmaf(CV(acc[3]), __high2float(p23), o[3]);
+#undef CV
+                }
+            }
         } else {
             // 32x32x32: a wave tile of 64x64 = 2x2 blocks; k = 128 = 4 MFMAs per block
 #pragma unroll
@@ -136,7 +160,7 @@ static void run(const char *name) {
     hipEventElapsedTime(&ms, e0, e1);
     long long c;
     hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-    const int mfma_per_iter = MODE == 2 ? 16 : 32;            // per wave
+    const int mfma_per_iter = MODE == 2 ? 16 : 32;  // (modes 3-5: 16x16 like 1)            // per wave
     const double macs = (double)256 * waves * iters * 16 * 16 * 128 * 16;  // 16 blocks of 16x16x128 (or 4 of 32x32x128)
     const double wps = waves / 4.0;                            // waves per SIMD
     printf("%-28s waves/SIMD=%.0f  cycles/iter/wave=%7.1f  SIMD cycles per 16x16x128 block=%6.1f (ideal 32)  TOPS=%7.1f\n",
@@ -151,7 +175,8 @@ int main() {
     run<0, 8>("mfma only 16x16x64");
     run<1, 8>("16x16x64 + dequant");
     run<2, 8>("32x32x32 + dequant");
-    run<1, 12>("16x16x64 + dequant");
-    run<2, 12>("32x32x32 + dequant");
+    run<3, 8>("16x16: cvt + fma_mix (no pk_mul)");
+    run<4, 8>("16x16: fma_mix + pk_mul (no cvt)");
+    run<5, 8>("16x16: fma_mix only");
     return 0;
 }
