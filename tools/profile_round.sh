@@ -5,7 +5,7 @@ R=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof gpurun_out/profiles
 P=gpurun_out/profiles  # merged back by gpurun; copy into profiles/ afterwards
-B="python3 bench.py --cpu-budget 0 --no-fp16-compare"
+B="python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers"
 # 1. kernel trace + stats of the default bench (LLaMA-2-7B, M=1)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/kt -o run -- $B --steps 5 > gpurun_out/prof/kt.log 2>&1
 cp gpurun_out/prof/kt/run_kernel_stats.csv $P/${R}_kernel_stats.csv
@@ -35,9 +35,10 @@ cp gpurun_out/prof/pf.log $P/${R}_prefill_bench.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/c5 -o run -- $B --config llama3-8b-prefill --steps 2 --warmup 1 --no-calibrate > gpurun_out/prof/c5.log 2>&1
 python3 tools/trace_summary.py gpurun_out/prof/c5/run_kernel_trace.csv > $P/${R}_c5_kernel_trace_summary.txt
 grep '"metric"' gpurun_out/prof/c5.log | tail -1 > $P/${R}_c5_bench_under_rocprof.json
-# 5. prefill PMC passes (one GEMM shape) and their per-dispatch averages
-rm -rf gpurun_out/pf1 gpurun_out/pf2 gpurun_out/pf3 gpurun_out/pf4
+# 5. prefill PMC passes (one GEMM shape, the U8 big-tile kernel) and their per-dispatch averages
+rm -rf gpurun_out/pf0 gpurun_out/pf1 gpurun_out/pf2 gpurun_out/pf3 gpurun_out/pf4 gpurun_out/pf5
 bash tools/pfprof.sh
-for i in 1 2 3 4; do python3 tools/pmc_avg.py gpurun_out/pf$i fq_gemm_prefill_kernel; done > $P/${R}_prefill_pmc.txt
+for i in 0 5 1 2 3 4; do python3 tools/pmc_avg.py gpurun_out/pf$i fq_gemm_prefill; done > $P/${R}_prefill_pmc.txt
 grep "TOPS" gpurun_out/pf1.log | tail -1 >> $P/${R}_prefill_pmc.txt
+python3 tools/pmc_summary.py gpurun_out/pf0/p_counter_collection.csv fq_gemm_prefill prefill-16384x4096x4096 $P/${R}_prefill_fetch_summary.json > /dev/null
 echo profiles done
