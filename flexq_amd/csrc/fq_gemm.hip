@@ -14,6 +14,7 @@
 // sum; C/D: col = l&15, row = 4*(l>>4) + r, r = 0..3 (cdna_hip_programming.md §3).  The fq6
 // weight layout stores exactly these B operands (16-column tiles, fq_quant.hip).
 #include "fq_lds.h"
+#include <cstdlib>
 
 // =============================================================================================
 // Decode / small-M kernel (M <= 32): HBM-bound weight streaming.
@@ -964,7 +965,8 @@ static size_t decode_lds_bytes(const DecodePlan &p, int M, int N, int K) {
 // Cost model, in quarter-blocks of one wave's stream (one 1.5 KiB block per wave at the
 // whole-chip rate is ~0.7 us for the 7B shapes; tools/fuse_bench.py, tools/stamps.py):
 //   stream   4 x items per WG x groups per wave
-//   k-split  12 (fix-up round trip, 1.1-1.7 us) + the slab bytes each WG writes and reads
+//   k-split  24 (the fix-up: slab drain, ticket and slab round trips, ~2.5 us; fitted to a forced-S
+//            sweep of the TP shard shapes, tools/ksplit_sweep.sh) + the slab bytes each WG moves
 //   fused    1 per (group, row) pair a wave quantizes (~0.17 us each, measured M = 1..16)
 //   split    12 for the separate quantize launch (~2.2 us incl. its launch)
 static const int kSplitQuantCost4 = 12;
@@ -990,12 +992,18 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused) {
         const long ipw = (items + grid - 1) / grid;
         const long ngw = ((G + S - 1) / S + NW - 1) / NW;
         long cost = 4 * ipw * ngw;
-        if (S > 1) cost += 12 + 4 * ipw * M * 128 / (NW * FQ_BLOCK);
+        if (S > 1) cost += 24 + 4 * ipw * M * 128 / (NW * FQ_BLOCK);
         if (best < 0 || cost < best) {
             best = cost;
             p.S = S;
         }
     }
+#ifdef FQ_DEV_ABLATION
+    if (const char *fs = getenv("FQ_DEV_S")) {  // development: force the k-split (tools/shape_sweep.py)
+        const int S = atoi(fs), items = NT * S, grid = items < cus ? items : cus;
+        if (S >= 1 && S <= G && grid % S == 0) p.S = S;
+    }
+#endif
     const int ngw = ((G + p.S - 1) / p.S + NW - 1) / NW;
     p.cost4 = (int)best + (fused ? ngw * M : kSplitQuantCost4);
     const int items = NT * p.S;
@@ -1065,7 +1073,6 @@ extern "C" fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_
 }
 
 #ifdef FQ_DEV_ABLATION
-#include <cstdlib>
 extern "C" int fq_dev_stamps(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fq_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
