@@ -763,7 +763,10 @@ constexpr int PB_WS_OFF = PB_XS_OFF + PB_BM * 4;     // w-scales of the 16 tiles
 constexpr int PB_ASTAGE = PB_WS_OFF + PB_TILES * 32; // 33.5 KiB
 constexpr int PB_BSTAGE = PB_TILES * 2 * 1024;       // unpacked B: [tile][k-step][lane][16 B]
 
-template <bool DBG>
+// ABL: development ablations as in fq_gemm_prefill_kernel (1, 2, 4, 8, 16).  XSF (M % 256 == 0:
+// every row tile full, its x-scales 16-byte aligned): the 256 x-scales of a group arrive packed in
+// one 512-byte DMA piece instead of four 64-lane ushort pieces into dword slots.
+template <bool DBG, int ABL = 0, bool XSF = false>
 __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
     int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu) {
@@ -805,13 +808,18 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
         usrc[t] = wu + (size_t)ut * G * 2048 + lane * 16;
     }
     auto stage = [&](int g, int slot) {
+        if (ABL & 8) return;
         char *buf = sa + slot * PB_ASTAGE;
 #pragma unroll
         for (int i = 0; i < 4; i++)
             __builtin_amdgcn_global_load_lds(asrc[i] + g * FQ_GROUP, LDS_PTR(buf + (32 * wid + 8 * i) * FQ_GROUP), 16, 0, 0);
-        if (wid < 4)
+        if (XSF) {
+            if (wid == 5 && lane < 32)
+                __builtin_amdgcn_global_load_lds(xs + (size_t)g * M + m0 + 8 * lane, LDS_PTR(buf + PB_XS_OFF), 16, 0, 0);
+        } else if (wid < 4) {
             __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PB_XS_OFF + 64 * wid * 4), 2, 0, 0);
-        else if (wid == 4 && lane < 32)
+        }
+        if (wid == 4 && lane < 32)
             __builtin_amdgcn_global_load_lds(wsrc + g * 16, LDS_PTR(buf + PB_WS_OFF), 16, 0, 0);
         char *bdst = sbu + slot * PB_BSTAGE + 2 * wid * 2048;
 #pragma unroll
@@ -824,7 +832,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     const uint32_t la = lds_addr(sa), lbu = lds_addr(sbu);
     const int arow = wm * 128 + (lane & 15);
     const uint32_t a_off0 = arow * FQ_GROUP + xswz(arow, lane >> 4), a_off1 = arow * FQ_GROUP + xswz(arow, 4 + (lane >> 4));
-    const uint32_t x_off = PB_XS_OFF + arow * 4;
+    const uint32_t x_off = PB_XS_OFF + arow * (XSF ? 2 : 4);
     const uint32_t w_off = PB_WS_OFF + (wn * 64 + 4 * (lane >> 4)) * 2;
     const uint32_t b_off = wn * 4 * 2048 + lane * 16;
 
@@ -848,6 +856,18 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
         v2u wv[4];
         v4i a[3][2];  // row blocks mi, mi + 1 and mi + 2 in flight
         uint32_t xv[3];
+        if (ABL & 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                b[i][0] = b[i][1] = v4i{(int)ab, (int)bb, g, i};
+                wv[i] = v2u{ab + i, bb};
+            }
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                a[i][0] = a[i][1] = v4i{(int)bb, (int)ab, i, g};
+                xv[i] = ab + 3 * i;
+            }
+        } else {
 #define FQ_PB_B(ni)                                                \
         b[ni][0] = ds_read_b128_at<(ni) * 2048>(bb);                \
         b[ni][1] = ds_read_b128_at<(ni) * 2048 + 1024>(bb);         \
@@ -857,7 +877,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
 #define FQ_PB_A(mi)                                                                  \
         a[(mi) % 3][0] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off0);          \
         a[(mi) % 3][1] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off1);          \
-        xv[(mi) % 3] = ds_read_b32_at<(mi) * 64>(ab + x_off);
+        xv[(mi) % 3] = XSF ? ds_read_u16_at<(mi) * 32>(ab + x_off) : ds_read_b32_at<(mi) * 64>(ab + x_off);
         FQ_PB_A(0) FQ_PB_A(1)
         // in flight: B (8) + w-scales (4) + rows 0, 1 (3 each); each row block's reads are waited
         // for with the next-but-one block's (3) and the next one's (3) still outstanding
@@ -865,6 +885,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                      : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]),
                        "+v"(b[3][0]), "+v"(b[3][1]), "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]),
                        "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
+        }
 #pragma unroll
         for (int mi = 0; mi < 8; mi++) {
             const int c = mi % 3;
@@ -875,19 +896,29 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
             }
             // issue row block mi + 2 into the slot row block mi - 1 used (its MFMAs are issued)
-            if (mi + 2 < 8) {
+            if (mi + 2 < 8 && !(ABL & 4)) {
                 const int c2 = (mi + 2) % 3;
                 const uint32_t ro = (mi + 2) * 16 * FQ_GROUP;
                 a[c2][0] = ds_read_b128(ab + a_off0 + ro);
                 a[c2][1] = ds_read_b128(ab + a_off1 + ro);
-                xv[c2] = ds_read_b32_at<0>(ab + x_off + (mi + 2) * 64);
+                xv[c2] = XSF ? ds_read_u16_at<0>(ab + x_off + (mi + 2) * 32) : ds_read_b32_at<0>(ab + x_off + (mi + 2) * 64);
             }
             const uint32_t x2u = __builtin_amdgcn_perm(xv[c], xv[c], 0x01000100u);  // half2(xs, xs)
             const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
 #pragma unroll
             for (int ni = 0; ni < 4; ni++) {
-                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[c][0], v4i{0, 0, 0, 0}, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[c][1], acc, 0, 0, 0);
+                v4i acc;
+                if (ABL & 2) {  // (development: operands kept alive, no MFMA)
+                    acc = b[ni][0] ^ a[c][1];
+                    asm volatile("" : "+v"(acc) : "v"(b[ni][1]), "v"(a[c][0]));
+                } else {
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[c][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[c][1], acc, 0, 0, 0);
+                }
+                if (ABL & 1) {  // (development: accumulators kept alive, no dequant)
+                    asm volatile("" ::"v"(acc), "v"(x2u), "v"(wv[ni]));
+                    continue;
+                }
                 const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
                 const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);  // fp16-rounded
                 const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);  // scale product
@@ -909,24 +940,43 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
         __builtin_amdgcn_s_waitcnt(vmcnt_only(0));  // stage g + 1 landed
     }
 
-    const bool vec = (N & 3) == 0;
+    // Epilogue: a lane holds 4 consecutive columns of each 16 x 16 block; one v_permlane16_swap per
+    // dword over the block pairs (0, 1), (2, 3) gives every lane 8 consecutive columns of one block
+    // (even 16-lane rows: block np, columns 8 (h >> 1) ..; odd rows: block np + 1), so the output
+    // leaves in 16-byte stores: 16 instead of 32 per lane.  The store tail of a one-WG-per-CU
+    // kernel is issue-bound (cdna_hip_programming.md T21), and every CU hits it at once.
+    const bool vec8 = (N & 7) == 0;
+    const int hrow = lane >> 4;
 #pragma unroll
     for (int mi = 0; mi < 8; mi++) {
         const int m = m0 + arow + mi * 16;
-        if (m >= M) continue;
 #pragma unroll
-        for (int ni = 0; ni < 4; ni++) {
-            const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
-            const float *o = out[mi][ni];
-            uint16_t *dst = d + (size_t)m * N + n;
-            if (vec && n + 3 < N) {
-                const uint32_t lo = (uint32_t)f2h(o[0] * 0.25f) | ((uint32_t)f2h(o[1] * 0.25f) << 16);
-                const uint32_t hi = (uint32_t)f2h(o[2] * 0.25f) | ((uint32_t)f2h(o[3] * 0.25f) << 16);
-                *reinterpret_cast<uint2 *>(dst) = make_uint2(lo, hi);
-            } else {
+        for (int np = 0; np < 4; np += 2) {
+            uint32_t pk[2][2];  // [block np + q][dword]: fp16 x 2, this lane's columns in order
 #pragma unroll
-                for (int r = 0; r < 4; r++)
-                    if (n + r < N) dst[r] = f2h(o[r] * 0.25f);
+            for (int q = 0; q < 2; q++) {
+                const float *o = out[mi][np + q];
+                pk[q][0] = (uint32_t)f2h(o[0] * 0.25f) | ((uint32_t)f2h(o[1] * 0.25f) << 16);
+                pk[q][1] = (uint32_t)f2h(o[2] * 0.25f) | ((uint32_t)f2h(o[3] * 0.25f) << 16);
+            }
+#pragma unroll
+            for (int w = 0; w < 2; w++) {
+                const auto r = __builtin_amdgcn_permlane16_swap(pk[0][w], pk[1][w], false, false);
+                pk[0][w] = r[0];
+                pk[1][w] = r[1];
+            }
+            const int n = (t0 + wn * 4 + np + (hrow & 1)) * 16 + 8 * (hrow >> 1);
+            if (ABL & 16) {
+                asm volatile("" ::"v"(pk[0][0]), "v"(pk[0][1]), "v"(pk[1][0]), "v"(pk[1][1]));
+            } else if (m < M) {
+                uint16_t *dst = d + (size_t)m * N + n;
+                if (vec8 && n + 7 < N) {
+                    *reinterpret_cast<uint4 *>(dst) = make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 8; r++)
+                        if (n + r < N) dst[r] = (uint16_t)(pk[r >> 2][(r >> 1) & 1] >> (16 * (r & 1)));
+                }
             }
         }
     }
@@ -1213,6 +1263,24 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
+    if (!acc_dbg && dev_ablation() >= 129 && dev_ablation() <= 159 && M >= PF_U8_MIN_M && workspace &&
+        workspace_bytes >= kTicketBytes + prefill_u8_bytes(N, K)) {  // the 256 x 256 kernel, ABL = value - 128
+        const int abl = dev_ablation() - 128;
+        char *wu = (char *)workspace + kTicketBytes;
+        const long nblk = (long)NT * (K / FQ_GROUP);
+        hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0, s,
+                           (const char *)w_packed, nblk, wu);
+        const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
+        const size_t lds_big = 2 * (size_t)(PB_ASTAGE + PB_BSTAGE);
+#define FQ_BABL(v)                                                                                         \
+        if (abl == v)                                                                                        \
+            hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<false, v>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
+        FQ_BABL(1) FQ_BABL(2) FQ_BABL(3) FQ_BABL(4) FQ_BABL(8) FQ_BABL(12) FQ_BABL(16) FQ_BABL(7) FQ_BABL(15)
+#undef FQ_BABL
+        FQ_LAUNCH_CHECK();
+        return FQ_OK;
+    }
 #endif
     // Large M with room in the workspace: unpack once, then the U8 kernel (without a workspace the
     // GEMM unpacks per WG; both are bit-identical)
@@ -1225,12 +1293,16 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
                            (const char *)w_packed, nblk, wu);
         const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
         const size_t lds_big = 2 * (size_t)(PB_ASTAGE + PB_BSTAGE);
-        if (acc_dbg)
-            hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<true>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s,
-                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
-        else
-            hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<false>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s,
-                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
+        const bool xsf = M % PB_BM == 0;
+#define FQ_BIG(dbg, xf)                                                                                    \
+        hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
+                           xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu)
+        if (acc_dbg) {
+            if (xsf) FQ_BIG(true, true); else FQ_BIG(true, false);
+        } else {
+            if (xsf) FQ_BIG(false, true); else FQ_BIG(false, false);
+        }
+#undef FQ_BIG
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }

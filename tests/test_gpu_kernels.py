@@ -426,7 +426,7 @@ def test_workspace_growth_keeps_captured_graphs_valid(ops, dev):
     del junk
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (4096, 4096, 4096)])
+@pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (2304, 1004, 1280), (4096, 4096, 4096)])
 def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     """Large M with a workspace: the weights are unpacked once (fq_unpack_w8_kernel) and the GEMM
     streams int8 operands (fq_gemm_prefill_kernel<U8>); without a workspace the GEMM unpacks per

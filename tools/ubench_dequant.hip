@@ -95,6 +95,73 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
 #undef CV
                 }
             }
+        } else if (MODE == 6) {
+            // 16x16x64, software-pipelined: block b's two MFMAs are interleaved with the dequant of
+            // block b - 1 (sched_group_barrier: 1 MFMA, 5 VALU, 1 MFMA, 5 VALU)
+            v4i accs[2];
+            accs[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[0][0], a[0][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+            accs[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[0][1], a[0][1], accs[0], 0, 0, 0);
+#pragma unroll
+            for (int bl = 1; bl <= 16; bl++) {
+                const int mi = bl >> 2, ni = bl & 3, pm = (bl - 1) >> 2, pn = (bl - 1) & 3;
+                if (bl < 16) {
+                    accs[bl & 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                    accs[bl & 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], accs[bl & 1], 0, 0, 0);
+                }
+                const v4i acc = accs[(bl - 1) & 1];
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[pm], xv[pm], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+                const uint32_t w01 = wv[pn][0], w23 = wv[pn][1];
+                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                float *o = out[pm][pn];
+                o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
+                o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
+                o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
+                o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
+                if (bl < 16) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+                }
+            }
+        } else if (MODE == 7) {
+            // 32x32x32 pipelined: the 4 MFMAs of block (mi, ni) interleaved with the dequant of the
+            // previous block (16 outputs: 16 cvt + 16 fma_mix + 8 pk_mul = 40 VALU, 10 per MFMA)
+            v16i accs[2];
+            auto mm = [&](int q, v16i c) {
+                const int mi = q >> 1, ni = q & 1;
+                c = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni][0], a[2 * mi][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni][1], a[2 * mi][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni + 1][0], a[2 * mi + 1][0], c, 0, 0, 0);
+                return __builtin_amdgcn_mfma_i32_32x32x32_i8(b[2 * ni + 1][1], a[2 * mi + 1][1], c, 0, 0, 0);
+            };
+            accs[0] = mm(0, v16i{});
+#pragma unroll
+            for (int q = 1; q <= 4; q++) {
+                if (q < 4) accs[q & 1] = mm(q, v16i{});
+                const int pm = (q - 1) >> 1, pn = (q - 1) & 1;
+                const v16i acc = accs[(q - 1) & 1];
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[pm], xv[pm], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const uint32_t w01 = wv[2 * pn + (r >> 1)][r & 1], w23 = wv[2 * pn + (r >> 1)][(r & 1) ^ 1];
+                    const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                    const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                    float *o = &out32[pm][pn][4 * r];
+                    o[0] = fmaf((float)acc[4 * r + 0], __low2float(p01), o[0]);
+                    o[1] = fmaf((float)acc[4 * r + 1], __high2float(p01), o[1]);
+                    o[2] = fmaf((float)acc[4 * r + 2], __low2float(p23), o[2]);
+                    o[3] = fmaf((float)acc[4 * r + 3], __high2float(p23), o[3]);
+                }
+                if (q < 4)
+                    for (int k = 0; k < 4; k++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+                    }
+            }
         } else {
             // 32x32x32: a wave tile of 64x64 = 2x2 blocks; k = 128 = 4 MFMAs per block
 #pragma unroll
@@ -160,7 +227,7 @@ static void run(const char *name) {
     hipEventElapsedTime(&ms, e0, e1);
     long long c;
     hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-    const int mfma_per_iter = MODE == 2 ? 16 : 32;  // (modes 3-5: 16x16 like 1)            // per wave
+    const int mfma_per_iter = (MODE == 2 || MODE == 7) ? 16 : 32;  // (modes 3-5: 16x16 like 1)            // per wave
     const double macs = (double)256 * waves * iters * 16 * 16 * 128 * 16;  // 16 blocks of 16x16x128 (or 4 of 32x32x128)
     const double wps = waves / 4.0;                            // waves per SIMD
     printf("%-28s waves/SIMD=%.0f  cycles/iter/wave=%7.1f  SIMD cycles per 16x16x128 block=%6.1f (ideal 32)  TOPS=%7.1f\n",
@@ -169,6 +236,15 @@ static void run(const char *name) {
 }
 
 int main() {
+    run<6, 4>("16x16 pipelined");
+    run<7, 4>("32x32 pipelined");
+    run<6, 8>("16x16 pipelined");
+    run<7, 8>("32x32 pipelined");
+    run<0, 16>("mfma only 16x16x64");
+    run<1, 16>("16x16x64 + dequant");
+    run<2, 16>("32x32x32 + dequant");
+    run<6, 16>("16x16 pipelined");
+    run<7, 16>("32x32 pipelined");
     run<0, 4>("mfma only 16x16x64");
     run<1, 4>("16x16x64 + dequant");
     run<2, 4>("32x32x32 + dequant");
