@@ -787,46 +787,46 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     const int bm = first + (lid % span) % gsz, bn = (lid % span) / gsz;
     const int m0 = bm * PB_BM, t0 = bn * PB_TILES;
 
-    // per-lane DMA sources at group 0: wave w stages A rows 32 w .. 32 w + 31 (4 pieces), the
-    // unpacked B of tiles 2 w, 2 w + 1 (4 pieces); waves 0-3 the x-scales of 64 rows each, wave 4
-    // the w-scales of the 16 tiles
-    const int8_t *asrc[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int row = 32 * wid + 8 * i + (lane >> 3);
-        const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M are computed, never stored
-        asrc[i] = xq + (size_t)m * K + ((lane & 7) ^ (row & 7)) * 16;
-    }
-    const int srow = 64 * (wid & 3) + lane;
+    // DMA: waves 4-7 issue all of it (wave 4 + v: A rows 64 v .. 64 v + 63 in 8 pieces, the unpacked
+    // B of tiles 4 v .. 4 v + 3 in 8, the x-scales (one packed piece from wave 5, XSF; otherwise 64
+    // rows per wave), wave 4 the w-scales); waves 0-3 issue none.  Waves w and w + 4 share a SIMD
+    // and otherwise run in lockstep (MI355X_MICROARCH.md, two waves per SIMD): this way waves 0-3
+    // reach their LDS reads and MFMAs while their partners are still issuing the next stage.
+    const bool dmaw = wid >= 4;
+    const int v4 = wid & 3;
+    const int swz = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;  // (row & 7 == (lane >> 3) & 7 for all 8 pieces)
+    const int srow = 64 * v4 + lane;
     const uint16_t *xsrc = xs + (m0 + srow < M ? m0 + srow : M - 1);
     const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;
     const uint16_t *wsrc = wsb + (size_t)wt * G * 16 + 8 * (lane & 1);
-    const char *usrc[2];
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-        const int ut = t0 + 2 * wid + t < NT ? t0 + 2 * wid + t : NT - 1;
-        usrc[t] = wu + (size_t)ut * G * 2048 + lane * 16;
-    }
     auto stage = [&](int g, int slot) {
         if (ABL & 8) return;
+        if (!dmaw) return;
         char *buf = sa + slot * PB_ASTAGE;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            __builtin_amdgcn_global_load_lds(asrc[i] + g * FQ_GROUP, LDS_PTR(buf + (32 * wid + 8 * i) * FQ_GROUP), 16, 0, 0);
+        for (int i = 0; i < 8; i++) {
+            const int row = 64 * v4 + 8 * i + (lane >> 3);
+            const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M are computed, never stored
+            __builtin_amdgcn_global_load_lds(xq + (size_t)m * K + g * FQ_GROUP + swz,
+                                             LDS_PTR(buf + (64 * v4 + 8 * i) * FQ_GROUP), 16, 0, 0);
+        }
         if (XSF) {
             if (wid == 5 && lane < 32)
                 __builtin_amdgcn_global_load_lds(xs + (size_t)g * M + m0 + 8 * lane, LDS_PTR(buf + PB_XS_OFF), 16, 0, 0);
-        } else if (wid < 4) {
-            __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PB_XS_OFF + 64 * wid * 4), 2, 0, 0);
+        } else {
+            __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PB_XS_OFF + 64 * v4 * 4), 2, 0, 0);
         }
         if (wid == 4 && lane < 32)
             __builtin_amdgcn_global_load_lds(wsrc + g * 16, LDS_PTR(buf + PB_WS_OFF), 16, 0, 0);
-        char *bdst = sbu + slot * PB_BSTAGE + 2 * wid * 2048;
+        char *bdst = sbu + slot * PB_BSTAGE + 4 * v4 * 2048;
 #pragma unroll
-        for (int t = 0; t < 2; t++)
+        for (int t = 0; t < 4; t++) {
+            const int ut = t0 + 4 * v4 + t < NT ? t0 + 4 * v4 + t : NT - 1;
+            const char *src = wu + ((size_t)ut * G + g) * 2048 + lane * 16;
 #pragma unroll
             for (int k = 0; k < 2; k++)
-                __builtin_amdgcn_global_load_lds(usrc[t] + (size_t)g * 2048 + k * 1024, LDS_PTR(bdst + t * 2048 + k * 1024), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(src + k * 1024, LDS_PTR(bdst + t * 2048 + k * 1024), 16, 0, 0);
+        }
     };
 
     const uint32_t la = lds_addr(sa), lbu = lds_addr(sbu);
