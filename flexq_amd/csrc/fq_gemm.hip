@@ -793,6 +793,9 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     // and otherwise run in lockstep (MI355X_MICROARCH.md, two waves per SIMD): this way waves 0-3
     // reach their LDS reads and MFMAs while their partners are still issuing the next stage.
     const bool dmaw = wid >= 4;
+    // Static priority for the DMA waves (measured: -2..-5 % against none or waves 0-3 prioritised):
+    // their next stage leaves earlier, and they are the later-dispatched, arbitration-losing half.
+    if (dmaw) __builtin_amdgcn_s_setprio(1);
     const int v4 = wid & 3;
     const int swz = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;  // (row & 7 == (lane >> 3) & 7 for all 8 pieces)
     const int srow = 64 * v4 + lane;
