@@ -665,8 +665,9 @@ def main():
         res["rehearsal"] = "--share-gpu: all ranks on one GPU, gloo with host-staged gathers (not a valid result)"
     if prefill and tp == 1:
         ach = ops_launch / per_gemm_s / 1e12
+        bytes_pf = int(layers * sum(alg_bytes(M, N, K, ab, False) for (_, N, K, ab) in launch_lins) / n_lin)
         res["roofline"] = {
-            "kernel": "fq_gemm_prefill_kernel",
+            "kernel": "fq_gemm_prefill_big_kernel" if M >= 2048 else "fq_gemm_prefill_kernel",
             "bound": "mfma",
             "achieved": round(ach, 1),
             "peak": I8_MFMA_PEAK_TOPS,
@@ -674,10 +675,10 @@ def main():
             "frac": round(ach / I8_MFMA_PEAK_TOPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "traffic_over_alg": round(traffic / bytes_pf, 4) if traffic else None,
             "per_launch_us": round(per_gemm_s * 1e6, 3),
             "alg_ops_per_launch": ops_launch,
-            "alg_bytes_per_launch": int(layers * sum(alg_bytes(M, N, K, ab, False)
-                                                     for (_, N, K, ab) in launch_lins) / n_lin),
+            "alg_bytes_per_launch": bytes_pf,
             "step_ms_linears_incl_quantize": round(elapsed / a.steps * 1e3, 4),
             "method": "graph of the step's prefill GEMM launches on pre-quantized codes (the quantize "
                       "launches excluded), HIP events on the capture stream; TOPS = 2*M*N*K / launch time",

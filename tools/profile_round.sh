@@ -35,6 +35,21 @@ cp gpurun_out/prof/pf.log $P/${R}_prefill_bench.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/c5 -o run -- $B --config llama3-8b-prefill --steps 2 --warmup 1 --no-calibrate > gpurun_out/prof/c5.log 2>&1
 python3 tools/trace_summary.py gpurun_out/prof/c5/run_kernel_trace.csv > $P/${R}_c5_kernel_trace_summary.txt
 grep '"metric"' gpurun_out/prof/c5.log | tail -1 > $P/${R}_c5_bench_under_rocprof.json
+# 4b. C5 HBM traffic: FETCH_SIZE pass over the prefill GEMM launches of the C5 bench (roofline.traffic)
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_prefill -f csv -d gpurun_out/prof/c5pmc -o run -- $B --config llama3-8b-prefill --steps 1 --warmup 1 --roofline-reps 1 --no-calibrate > gpurun_out/prof/c5pmc.log 2>&1
+cp gpurun_out/prof/c5pmc/run_counter_collection.csv $P/${R}_c5_pmc_fetch_size.csv
+python3 tools/pmc_summary.py $P/${R}_c5_pmc_fetch_size.csv fq_gemm_prefill llama3-8b-prefill $P/${R}_c5_pmc_summary.json > /dev/null
+python3 - "$R" <<'PY'
+import json, sys
+p = f"gpurun_out/profiles/{sys.argv[1]}_c5_pmc_summary.json"
+d = json.load(open(p))
+d.update(merged_gate_up=True, launch_pattern="qkv, o, gate_up (merged), down per layer; the prefill GEMM launches only",
+         command="rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_prefill -f csv -- "
+                 "python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers --config llama3-8b-prefill "
+                 "--steps 1 --warmup 1 --roofline-reps 1 --no-calibrate")
+d["source"] = f"profiles/{sys.argv[1]}_c5_pmc_fetch_size.csv"
+json.dump(d, open(p, "w"), indent=1)
+PY
 # 5. prefill PMC passes (one GEMM shape, the U8 big-tile kernel) and their per-dispatch averages
 rm -rf gpurun_out/pf0 gpurun_out/pf1 gpurun_out/pf2 gpurun_out/pf3 gpurun_out/pf4 gpurun_out/pf5
 bash tools/pfprof.sh
