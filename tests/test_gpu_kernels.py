@@ -426,6 +426,45 @@ def test_workspace_growth_keeps_captured_graphs_valid(ops, dev):
     del junk
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 512, 8192), (4, 1024, 28672), (16, 2048, 28672)])
+def test_split_k_back_to_back_graph_replay(ops, dev, M, N, K):
+    """The cross-workgroup split-K hand-off (write-through slabs, one agent-scope ticket per tile,
+    last arriver sums) under back-to-back launches: a graph of 48 launches over 4 inputs and 3
+    weight images (tickets reused every launch, consumers on every XCD, uneven arrival), replayed
+    4 times; every output bit-identical to its eager launch.  (A mid-stream ticket poll passed a few
+    eager calls and hung under exactly this replay pattern)"""
+    from flexq_amd import _lib
+    assert _lib.load().fq_gemm_workspace_bytes(M, N, K) > 0  # the plan splits K
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    xs = [torch.randn((M, K), dtype=torch.float16, device=dev, generator=g) for _ in range(4)]
+    pks = [ops.pack_w6(torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g),
+                       (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()) for _ in range(3)]
+    R = 48
+    pairs = [(i % 4, i % 3) for i in range(R)]
+    outs = [torch.empty((M, N), dtype=torch.float16, device=dev) for _ in range(R)]
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        for i, (a, b) in enumerate(pairs):
+            ops.linear_w6ax(xs[a], pks[b], N, 6, out=outs[i])
+    torch.cuda.synchronize()
+    want = [o.clone() for o in outs]
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        for i, (a, b) in enumerate(pairs):
+            ops.linear_w6ax(xs[a], pks[b], N, 6, out=outs[i])
+    for _ in range(4):
+        for o in outs:
+            o.fill_(-1)
+        graph.replay()
+        torch.cuda.synchronize()
+        for i in range(R):
+            assert torch.equal(outs[i].view(torch.int16), want[i].view(torch.int16)), f"launch {i}"
+    # and the eager results agree across inputs that share an (x, W) pair
+    for i in range(R):
+        j = pairs.index(pairs[i])
+        assert torch.equal(want[i].view(torch.int16), want[j].view(torch.int16))
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (2304, 1004, 1280), (4096, 4096, 4096)])
 def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     """Large M with a workspace: the weights are unpacked once (fq_unpack_w8_kernel) and the GEMM

@@ -37,15 +37,25 @@ def main():
             imgs.append(ops.pack_w6(wq, (torch.rand((K // 128, N), device=dev, generator=g) * 0.01).half()))
         x = torch.randn((M, K), device=dev, dtype=torch.float16, generator=g)
         out = torch.empty((M, N), device=dev, dtype=torch.float16)
+        mode = os.environ.get("FQ_SWEEP", "linear")  # linear | gemm (pre-quantized) | quant (quantizer only)
+        xq, xs = ops.quantize_act(x, 6)
+
+        def call(img):
+            if mode == "gemm":
+                ops.gemm_w6ax(xq, xs, img, N, 6, out=out)
+            elif mode == "quant":
+                ops.quantize_act(x, 6)
+            else:
+                ops.linear_w6ax(x, img, N, 6, out=out)
         ops.reserve_workspace(dev, [(M, N, K)], stream=stream)
         with torch.cuda.stream(stream):
             for c in imgs:
-                ops.linear_w6ax(x, c, N, 6, out=out)
+                call(c)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream):
             for i in range(R):
-                ops.linear_w6ax(x, imgs[i % copies], N, 6, out=out)
+                call(imgs[i % copies])
         graph.replay()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,7 +67,7 @@ def main():
             e.synchronize()
             best = min(best, s.elapsed_time(e) * 1e3 / R)
         nb = N * K * 0.75 + N * K / 64 + 2 * M * K + 2 * M * N
-        print(f"{os.environ.get('FQ_LIB', 'lib')} M={M} N={N:6d} K={K:6d} tiles/CU={N / 16 / 256:5.2f} us/launch={best:7.2f} TB/s={nb / best / 1e6:5.2f}",
+        print(f"{os.environ.get('FQ_LIB', 'lib')} {mode} M={M} N={N:6d} K={K:6d} tiles/CU={N / 16 / 256:5.2f} us/launch={best:7.2f} TB/s={nb / best / 1e6:5.2f}",
               flush=True)
         del imgs, graph
         torch.cuda.empty_cache()
