@@ -55,6 +55,28 @@ def test_null_and_shape_errors_are_status_codes():
     assert lib.fq_ref_bit_packing(P(16), P(16), 12, 128, 6, None) == 2         # rows 9..15 unsupported
 
 
+def test_missing_extension_fails_loudly():
+    """No CPU or eager fallback: with the shared object absent, every op raises
+    FlexQExtensionError (a fresh interpreter, so the already-loaded library is not reused)."""
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from flexq_amd import _lib\n"
+        "_lib.LIB_PATH = '/nonexistent/libflexq_hip.so'\n"
+        "from flexq_amd import ops\n"
+        "import torch\n"
+        "for fn in (lambda: _lib.load(), lambda: _lib.version(),\n"
+        "           lambda: ops.act_scratch_bytes(1, 4096, 4096)):\n"
+        "    try:\n"
+        "        fn()\n"
+        "    except _lib.FlexQExtensionError as e:\n"
+        "        assert 'not built' in str(e)\n"
+        "    else:\n"
+        "        raise SystemExit('no error')\n"
+        "print('raised')\n" % ROOT)
+    r = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "raised" in r.stdout, r.stdout + r.stderr
+
+
 def test_wrappers_reject_cpu_tensors():
     from flexq_amd import ops
     with pytest.raises(ValueError, match="HIP device"):
