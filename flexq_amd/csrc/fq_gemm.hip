@@ -763,7 +763,24 @@ constexpr int PB_WS_OFF = PB_XS_OFF + PB_BM * 4;     // w-scales of the 16 tiles
 constexpr int PB_ASTAGE = PB_WS_OFF + PB_TILES * 32; // 33.5 KiB
 constexpr int PB_BSTAGE = PB_TILES * 2 * 1024;       // unpacked B: [tile][k-step][lane][16 B]
 
-// ABL: development ablations as in fq_gemm_prefill_kernel (1, 2, 4, 8, 16).  XSF (M % 256 == 0:
+#ifdef FQ_DEV_ABLATION
+// development (ABL & 32): per-wave cycle sums of the group-step segments (barrier wait, stage DMA
+// issue, compute, trailing DMA wait) for the first 256 workgroups, tools/pb_stamps.py
+__device__ unsigned long long g_pb_stamps[256 * PB_WAVES * 4];
+#define PB_STAMP(k)                                                                          \
+    if (ABL & 32) {                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+        unsigned long long t_;                                                               \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+        if ((k) >= 0) pb_seg[(k) < 0 ? 0 : (k)] += t_ - pb_t;                                \
+        pb_t = t_;                                                                           \
+    }
+#else
+#define PB_STAMP(k)
+#endif
+
+// ABL: development ablations as in fq_gemm_prefill_kernel (1, 2, 4, 8, 16; 32 stamps).  XSF (M % 256 == 0:
 // every row tile full, its x-scales 16-byte aligned): the 256 x-scales of a group arrive packed in
 // one 512-byte DMA piece instead of four 64-lane ushort pieces into dword slots.
 template <bool DBG, int ABL = 0, bool XSF = false>
@@ -849,11 +866,18 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
 
     stage(0, 0);
     __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
+    unsigned long long pb_seg[4] = {0, 0, 0, 0}, pb_t = 0;
+    (void)pb_seg;
+    (void)pb_t;
+    PB_STAMP(-1);
     for (int g = 0; g < G; g++) {
+        PB_STAMP(3);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
+        PB_STAMP(0);
         stage(g + 1 < G ? g + 1 : G - 1, (g + 1) & 1);  // (past the last group: a never-read copy)
+        PB_STAMP(1);
         const uint32_t ab = la + (g & 1) * PB_ASTAGE, bb = lbu + (g & 1) * PB_BSTAGE + b_off;
         v4i b[4][2];
         v2u wv[4];
@@ -889,27 +913,50 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                        "+v"(b[3][0]), "+v"(b[3][1]), "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]),
                        "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
         }
+        // Blocks j = (mi, ni) in order, the dequant of block j - 1 after the MFMAs of block j: the
+        // accumulators' MFMA latency is covered by the next block's MFMAs instead of s_nops.
+        v4i accq[2];
+        __half2 x2s[2];  // the x-scale pair of row blocks mi (even / odd): the dequant of (mi, 3) runs
+                         // after row block mi + 1 has taken over the slot of xv
+        auto dequant = [&](const v4i acc, int mi, int ni) {
+            const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+            const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2s[mi & 1]);  // fp16-rounded
+            const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2s[mi & 1]);  // scale product
+            float *o = out[mi][ni];
+            o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
+            o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
+            o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
+            o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
+            if (DBG) {
+                const int m = m0 + arow + mi * 16;
+                const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
 #pragma unroll
-        for (int mi = 0; mi < 8; mi++) {
-            const int c = mi % 3;
-            if (mi > 0) {  // row block mi landed; mi + 1 may still be in flight
-                if (mi + 1 < 8)
-                    asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
-                else
-                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+                for (int r = 0; r < 4; r++)
+                    if (m < M && n + r < N) acc_dbg[((size_t)m * N + n + r) * G + g] = acc[r] >> 2;
             }
-            // issue row block mi + 2 into the slot row block mi - 1 used (its MFMAs are issued)
-            if (mi + 2 < 8 && !(ABL & 4)) {
-                const int c2 = (mi + 2) % 3;
-                const uint32_t ro = (mi + 2) * 16 * FQ_GROUP;
-                a[c2][0] = ds_read_b128(ab + a_off0 + ro);
-                a[c2][1] = ds_read_b128(ab + a_off1 + ro);
-                xv[c2] = XSF ? ds_read_u16_at<0>(ab + x_off + (mi + 2) * 32) : ds_read_b32_at<0>(ab + x_off + (mi + 2) * 64);
-            }
-            const uint32_t x2u = __builtin_amdgcn_perm(xv[c], xv[c], 0x01000100u);  // half2(xs, xs)
-            const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+        };
 #pragma unroll
-            for (int ni = 0; ni < 4; ni++) {
+        for (int j = 0; j <= 32; j++) {
+            if (j < 32) {
+                const int mi = j >> 2, ni = j & 3, c = mi % 3;
+                if (ni == 0) {
+                    if (mi > 0) {  // row block mi landed; mi + 1 may still be in flight
+                        if (mi + 1 < 8)
+                            asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+                        else
+                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+                    }
+                    // issue row block mi + 2 into the slot row block mi - 1 used (its MFMAs are issued)
+                    if (mi + 2 < 8 && !(ABL & 4)) {
+                        const int c2 = (mi + 2) % 3;
+                        const uint32_t ro = (mi + 2) * 16 * FQ_GROUP;
+                        a[c2][0] = ds_read_b128(ab + a_off0 + ro);
+                        a[c2][1] = ds_read_b128(ab + a_off1 + ro);
+                        xv[c2] = XSF ? ds_read_u16_at<0>(ab + x_off + (mi + 2) * 32) : ds_read_b32_at<0>(ab + x_off + (mi + 2) * 64);
+                    }
+                    const uint32_t x2u = __builtin_amdgcn_perm(xv[c], xv[c], 0x01000100u);  // half2(xs, xs)
+                    x2s[mi & 1] = *reinterpret_cast<const __half2 *>(&x2u);
+                }
                 v4i acc;
                 if (ABL & 2) {  // (development: operands kept alive, no MFMA)
                     acc = b[ni][0] ^ a[c][1];
@@ -918,30 +965,29 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[c][0], v4i{0, 0, 0, 0}, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[c][1], acc, 0, 0, 0);
                 }
-                if (ABL & 1) {  // (development: accumulators kept alive, no dequant)
-                    asm volatile("" ::"v"(acc), "v"(x2u), "v"(wv[ni]));
-                    continue;
-                }
-                const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
-                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);  // fp16-rounded
-                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);  // scale product
-                float *o = out[mi][ni];
-                o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
-                o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
-                o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
-                o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
-                if (DBG) {
-                    const int m = m0 + arow + mi * 16;
-                    const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        if (m < M && n + r < N) acc_dbg[((size_t)m * N + n + r) * G + g] = acc[r] >> 2;
-                }
+                accq[j & 1] = acc;
             }
+            // pinned order: this block's MFMAs, then the previous block's dequant (hipcc would hoist
+            // the dequant above the MFMAs and stall on the accumulators; measured 2-5 % faster)
+            __builtin_amdgcn_sched_barrier(0);
+            if (j > 0) {
+                const int pj = j - 1;
+                if (ABL & 1)  // (development: accumulators kept alive, no dequant)
+                    asm volatile("" ::"v"(accq[pj & 1]), "v"(x2s[(pj >> 2) & 1]), "v"(wv[pj & 3]));
+                else
+                    dequant(accq[pj & 1], pj >> 2, pj & 3);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
+        PB_STAMP(2);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(vmcnt_only(0));  // stage g + 1 landed
     }
+    PB_STAMP(3);
+#ifdef FQ_DEV_ABLATION
+    if ((ABL & 32) && lane == 0 && blockIdx.x < 256)
+        for (int k = 0; k < 4; k++) g_pb_stamps[(blockIdx.x * PB_WAVES + wid) * 4 + k] = pb_seg[k];
+#endif
 
     // Epilogue: a lane holds 4 consecutive columns of each 16 x 16 block; one v_permlane16_swap per
     // dword over the block pairs (0, 1), (2, 3) gives every lane 8 consecutive columns of one block
@@ -1129,6 +1175,9 @@ extern "C" fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_
 extern "C" int fq_dev_stamps(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fq_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
+extern "C" int fq_dev_pb_stamps(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pb_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
 static int dev_ablation() {
     const char *e = getenv("FQ_DEV_ABLATION");
     return e ? atoi(e) : 0;
@@ -1266,7 +1315,7 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
-    if (!acc_dbg && dev_ablation() >= 129 && dev_ablation() <= 159 && M >= PF_U8_MIN_M && workspace &&
+    if (!acc_dbg && dev_ablation() >= 129 && dev_ablation() <= 191 && M >= PF_U8_MIN_M && workspace &&
         workspace_bytes >= kTicketBytes + prefill_u8_bytes(N, K)) {  // the 256 x 256 kernel, ABL = value - 128
         const int abl = dev_ablation() - 128;
         char *wu = (char *)workspace + kTicketBytes;
@@ -1279,7 +1328,7 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         if (abl == v)                                                                                        \
             hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<false, v>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
                                xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
-        FQ_BABL(1) FQ_BABL(2) FQ_BABL(3) FQ_BABL(4) FQ_BABL(8) FQ_BABL(12) FQ_BABL(16) FQ_BABL(7) FQ_BABL(15)
+        FQ_BABL(1) FQ_BABL(2) FQ_BABL(3) FQ_BABL(4) FQ_BABL(8) FQ_BABL(12) FQ_BABL(16) FQ_BABL(7) FQ_BABL(15) FQ_BABL(32)
 #undef FQ_BABL
         FQ_LAUNCH_CHECK();
         return FQ_OK;
