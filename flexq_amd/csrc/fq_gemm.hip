@@ -674,43 +674,56 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
         asm volatile("s_waitcnt lgkmcnt(12)"
                      : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]),
                        "+v"(b[3][0]), "+v"(b[3][1]), "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]));
+        // Blocks j = (mi, ni) in order, the dequant of block j - 1 pinned after the MFMAs of block j
+        // (as in fq_gemm_prefill_big_kernel: the accumulators' latency is covered by those MFMAs)
+        v4i accq[2];
+        __half2 x2s[2];
+        auto dequant = [&](const v4i acc, int mi, int ni) {
+            const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+            const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2s[mi & 1]);  // fp16-rounded
+            const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2s[mi & 1]);  // scale product
+            float *o = out[mi][ni];
+            o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
+            o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
+            o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
+            o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
+            if (DBG) {
+                const int m = m0 + arow + mi * 16;
+                const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
 #pragma unroll
-        for (int mi = 0; mi < 4; mi++) {
-            if (mi == 0) asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
-            if (mi == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xv[1]));
-            if (mi == 2) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[2][0]), "+v"(a[2][1]), "+v"(xv[2]));
-            if (mi == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[3][0]), "+v"(a[3][1]), "+v"(xv[3]));
-            const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);  // half2(xs, xs)
-            const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+                for (int r = 0; r < 4; r++)
+                    if (m < M && n + r < N) acc_dbg[((size_t)m * N + n + r) * G + g] = acc[r] >> 2;
+            }
+        };
 #pragma unroll
-            for (int ni = 0; ni < 4; ni++) {
+        for (int j = 0; j <= 16; j++) {
+            if (j < 16) {
+                const int mi = j >> 2, ni = j & 3;
+                if (ni == 0) {
+                    if (mi == 0) asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
+                    if (mi == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xv[1]));
+                    if (mi == 2) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[2][0]), "+v"(a[2][1]), "+v"(xv[2]));
+                    if (mi == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[3][0]), "+v"(a[3][1]), "+v"(xv[3]));
+                    const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);  // half2(xs, xs)
+                    x2s[mi & 1] = *reinterpret_cast<const __half2 *>(&x2u);
+                }
                 if (ABL & 2) {
-                    asm volatile("" ::"v"(a[mi][0]), "v"(a[mi][1]), "v"(b[ni][0]), "v"(b[ni][1]), "v"(x2u), "v"(wv[ni]));
-                    continue;
-                }
-                // weights as the A operand: acc[r] = column 4 (lane >> 4) + r, row lane & 15
-                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
-                if (ABL & 1) {
-                    asm volatile("" ::"v"(acc), "v"(x2u), "v"(wv[ni]));
-                    continue;
-                }
-                const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
-                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);  // fp16-rounded
-                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);  // scale product
-                float *o = out[mi][ni];
-                o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
-                o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
-                o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
-                o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
-                if (DBG) {
-                    const int m = m0 + arow + mi * 16;
-                    const int n = (t0 + wn * 4 + ni) * 16 + 4 * (lane >> 4);
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        if (m < M && n + r < N) acc_dbg[((size_t)m * N + n + r) * G + g] = acc[r] >> 2;
+                    asm volatile("" ::"v"(a[mi][0]), "v"(a[mi][1]), "v"(b[ni][0]), "v"(b[ni][1]), "v"(x2s[mi & 1]), "v"(wv[ni]));
+                } else {
+                    // weights as the A operand: acc[r] = column 4 (lane >> 4) + r, row lane & 15
+                    v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
+                    accq[j & 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
+            if (j > 0 && !(ABL & 2)) {
+                const int pj = j - 1;
+                if (ABL & 1)
+                    asm volatile("" ::"v"(accq[pj & 1]), "v"(x2s[(pj >> 2) & 1]), "v"(wv[pj & 3]));
+                else
+                    dequant(accq[pj & 1], pj >> 2, pj & 3);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
         // A stage g + 1 landed (the weights of group g + 2 may stay in flight); the unpack writes
         // retired with the reads above.  (sched_barrier: keep the wait below the MFMA block.)
