@@ -504,7 +504,8 @@ __device__ __forceinline__ uint32_t ds_read_b32_at(uint32_t a) {
 template <bool DBG, int ABL = 0, bool U8 = false>
 __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
-    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu = nullptr) {
+    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu, int S,
+    float *__restrict__ slabs) {
     __shared__ __attribute__((aligned(16))) char sa[2 * PF_ASTAGE];
     __shared__ __attribute__((aligned(16))) char sbu[2 * PF_BSTAGE];
     __shared__ __attribute__((aligned(16))) char sraw[U8 ? 16 : PF_WAVES * 3072];
@@ -517,7 +518,11 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     // Block order: the bijective XCD remap (consecutive logical tiles run on one XCD), then groups
     // of 8 M-panels walked M-fastest, so the WGs resident on an XCD share A and B k-slices in L2.
     const int nbm = (M + PF_BM - 1) / PF_BM, nbn = (NT + PF_TILES - 1) / PF_TILES, nwg = nbm * nbn;
-    const int bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    // split-K (S > 1, few tiles): WG b takes tile b / S and groups [g0, g1) of split z = b % S
+    const int bid = S == 1 ? (int)blockIdx.x : (int)((unsigned)blockIdx.x / (unsigned)S);
+    const int z = (int)blockIdx.x - bid * S;
+    const int g0 = (int)((unsigned)(z * G) / (unsigned)S), g1 = (int)((unsigned)((z + 1) * G) / (unsigned)S);
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
     const int lid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
     const int span = 8 * nbn, first = (lid / span) * 8;
     const int gsz = nbm - first < 8 ? nbm - first : 8;
@@ -617,12 +622,12 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
             for (int r = 0; r < 4; r++) out[i][j][r] = 0.f;
 
     // prologue: A stage 0 and the weights of group 0; unpack them; weights of group 1
-    stage(0, 0);
+    stage(g0, 0);
     if (!U8) {
-        load_w(0);
+        load_w(g0);
         __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
         read_w();
-        load_w(G > 1 ? 1 : 0);
+        load_w(g1 > g0 + 1 ? g0 + 1 : g0);
         unpack_w(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
@@ -632,19 +637,20 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     // Step g: barrier (A stage g, B operands g in LDS; every wave done with step g - 1) -> issue A
     // stage g + 1 -> the weights of group g + 1 (loaded a step ago) to registers, their buffer
     // refilled with group g + 2, unpacked to LDS -> MFMAs on group g -> wait for A stage g + 1.
-    for (int g = 0; g < G; g++) {
+    for (int g = g0; g < g1; g++) {
+        const int gl = g - g0;  // stage parity
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        stage(g + 1 < G ? g + 1 : G - 1, (g + 1) & 1);  // past the last group: never-read copies,
-        if (!U8) {                                       // so every path issues the same count
+        stage(g + 1 < g1 ? g + 1 : g1 - 1, (gl + 1) & 1);  // past the last group: never-read copies,
+        if (!U8) {                                          // so every path issues the same count
             __builtin_amdgcn_s_waitcnt(vmcnt_only(PF_VM_A));
             read_w();
-            load_w(g + 2 < G ? g + 2 : G - 1);
-            unpack_w((g + 1) & 1);
+            load_w(g + 2 < g1 ? g + 2 : g1 - 1);
+            unpack_w((gl + 1) & 1);
         }
 
-        const uint32_t ab = la + (g & 1) * PF_ASTAGE, bb = lbu + (g & 1) * PF_BSTAGE + b_off;
+        const uint32_t ab = la + (gl & 1) * PF_ASTAGE, bb = lbu + (gl & 1) * PF_BSTAGE + b_off;
         v4i b[4][2];
         v2u wv[4];
         v4i a[4][2];
@@ -733,6 +739,22 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
     // the copies past the last group are still landing: LDS must be quiet before the WG retires
     __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
 
+    if (S > 1) {  // fp32 partial tile -> split z's slab [z][M][Npad]; fq_splitk_reduce_kernel sums them
+        const size_t Npad = (size_t)NT * 16;
+#pragma unroll
+        for (int mi = 0; mi < 4; mi++) {
+            const int m = m0 + arow + mi * 16;
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++) {
+                const int tn = t0 + wn * 4 + ni;
+                const float *o = out[mi][ni];
+                if (!(ABL & 16) && m < M && tn < NT)
+                    *reinterpret_cast<float4 *>(slabs + ((size_t)z * M + m) * Npad + tn * 16 + 4 * (lane >> 4)) =
+                        make_float4(o[0] * 0.25f, o[1] * 0.25f, o[2] * 0.25f, o[3] * 0.25f);
+            }
+        }
+        return;
+    }
     // 4 consecutive columns per lane: one 8-byte store when N keeps them 8-byte aligned
     const bool vec = (N & 3) == 0;
 #pragma unroll
@@ -757,6 +779,36 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
                 }
             }
         }
+    }
+}
+
+// Split-K finish: d = fp16(sum over z = 0 .. S-1 of slab z), in z order (deterministic), four
+// columns per thread.  Traffic: 4 S M Npad bytes read, 2 M N written.
+__global__ __launch_bounds__(256) void fq_splitk_reduce_kernel(const float *__restrict__ slabs, int S, int M, int N,
+                                                                uint16_t *__restrict__ d) {
+    const int NT = (N + 15) / 16, q4 = NT * 4;  // float4 columns per row
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long)M * q4) return;
+    const int m = (int)(idx / q4), c = (int)(idx - (long)m * q4);
+    const size_t stride = (size_t)M * NT * 16;
+    const float4 *src = reinterpret_cast<const float4 *>(slabs + (size_t)m * NT * 16) + c;
+    float4 v = src[0];
+    for (int zz = 1; zz < S; zz++) {
+        const float4 w = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(src) + zz * stride);
+        v.x += w.x;
+        v.y += w.y;
+        v.z += w.z;
+        v.w += w.w;
+    }
+    const int n = 4 * c;
+    uint16_t *dst = d + (size_t)m * N + n;
+    const uint16_t h[4] = {f2h(v.x), f2h(v.y), f2h(v.z), f2h(v.w)};
+    if ((N & 3) == 0 && n + 3 < N) {
+        *reinterpret_cast<uint2 *>(dst) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (n + r < N) dst[r] = h[r];
     }
 }
 
@@ -1166,10 +1218,45 @@ __global__ __launch_bounds__(256) void fq_unpack_w8_kernel(const char *__restric
     *reinterpret_cast<v4i *>(dst + 1024) = unpack_fq6(p0.y, p1.y, p2.y);
 }
 
+// Split-K for the 128 x 128 prefill kernel when its tiles leave the chip under-filled (32 < M <
+// PF_U8_MIN_M with few row x column tiles, e.g. M = 64, N = 4096: 32 WGs on 256 CUs).  Modelled
+// time in us: rounds of two WGs per CU (its occupancy) x groups per split x PF_STEP_US per group
+// step, plus for S > 1 the reduce launch and the fp32 slab bytes (written once, read once) at an
+// effective 3 TB/s.  Constants fitted to a forced-S sweep on MI355X (tools/psplit_sweep.sh: M = 33
+// .. 1024 on four LLaMA-2-7B shapes, 120 runs): the plan is within 2.1 us of the best S in every
+// case (5.2 us summed over 24; the first guess, one WG per CU at 1.3 us and 5 TB/s, lost 36).
+static const double PF_STEP_US = 1.4, PF_RED_US = 1.0, PF_SLAB_BPUS = 3e6;
+static int prefill_split(int M, int N, int K) {
+    if (M <= 32 || M >= PF_U8_MIN_M) return 1;
+    const int G = K / FQ_GROUP, NT = (N + 15) / 16;
+    const double nwg = (double)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES), slots = 2.0 * device_cus();
+    int bs = 1;
+    double best = 0;
+    for (int S = 1; S <= 16 && S <= G; S *= 2) {  // the calibrated splits: 1, 2, 4, 8, 16
+        const double t = ceil(nwg * S / slots) * ceil((double)G / S) * PF_STEP_US +
+                         (S > 1 ? PF_RED_US + 2.0 * S * M * NT * 16 * sizeof(float) / PF_SLAB_BPUS : 0.0);
+        if (S == 1 || t < best) {
+            best = t;
+            bs = S;
+        }
+    }
+#ifdef FQ_DEV_ABLATION
+    if (const char *fs = getenv("FQ_DEV_PS")) {  // development: force S (tools/psplit_sweep.sh)
+        const int f = atoi(fs);
+        if (f >= 1 && f <= G) bs = f;
+    }
+#endif
+    return bs;
+}
+static size_t prefill_slab_bytes(int M, int N, int S) { return (size_t)S * M * ((N + 15) / 16) * 16 * sizeof(float); }
+
 extern "C" size_t fq_gemm_workspace_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
     if (M >= PF_U8_MIN_M) return kTicketBytes + prefill_u8_bytes(N, K);  // tickets left untouched
-    if (M > 32) return 0;
+    if (M > 32) {
+        const int S = prefill_split(M, N, K);
+        return S > 1 ? kTicketBytes + prefill_slab_bytes(M, N, S) : 0;
+    }
     const int S = decode_plan(M, N, K, false).S;  // the same for every staging variant and fused
     if (S == 1) return 0;
     const size_t Npad = (size_t)((N + 15) / 16) * 16;
@@ -1318,10 +1405,10 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
 #define FQ_PABL(v)                                                                                         \
         if (abl == v && u8)                                                                                  \
             hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, v, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, \
-                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);        \
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr); \
         if (abl == v && !u8)                                                                                 \
             hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, v>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs, \
-                               (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
+                               (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr, 1, nullptr);
         FQ_PABL(1) FQ_PABL(2) FQ_PABL(3) FQ_PABL(4) FQ_PABL(5) FQ_PABL(7) FQ_PABL(8) FQ_PABL(11) FQ_PABL(15)
         FQ_PABL(16) FQ_PABL(31) FQ_PABL(35) FQ_PABL(67) FQ_PABL(99) FQ_PABL(6) FQ_PABL(12) FQ_PABL(17) FQ_PABL(19)
 #undef FQ_PABL
@@ -1371,12 +1458,23 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
+    // Few tiles (narrow N, modest M): split K over more WGs when the workspace holds the slabs
+    int S = prefill_split(M, N, K);
+    if (S > 1 && (!workspace || workspace_bytes < kTicketBytes + prefill_slab_bytes(M, N, S))) S = 1;
+    float *slabs = S > 1 ? reinterpret_cast<float *>((char *)workspace + kTicketBytes) : nullptr;
+    const unsigned grid = (unsigned)(nwg * S);
     if (acc_dbg)
-        hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs,
-                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
+        hipLaunchKernelGGL(fq_gemm_prefill_kernel<true>, dim3(grid), dim3(PF_WAVES * 64), 0, s, xq, xs,
+                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr, S, slabs);
     else
-        hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s, xq, xs,
-                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr);
+        hipLaunchKernelGGL(fq_gemm_prefill_kernel<false>, dim3(grid), dim3(PF_WAVES * 64), 0, s, xq, xs,
+                           (const uint32_t *)w_packed, M, N, K, d, acc_dbg, nullptr, S, slabs);
     FQ_LAUNCH_CHECK();
+    if (S > 1) {
+        const long nthr = (long)M * NT * 4;
+        hipLaunchKernelGGL(fq_splitk_reduce_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s,
+                           (const float *)slabs, S, M, N, d);
+        FQ_LAUNCH_CHECK();
+    }
     return FQ_OK;
 }

@@ -64,9 +64,11 @@ size_t fq_packed_w_bytes(int N, int K);
 /* Bytes of scratch fq_gemm_w6ax / fq_linear_w6ax need for this shape (0 if none).  The buffer
  * must be zero-filled once after allocation (fq_workspace_init).  Layout: a 256 KiB ticket
  * region (split-K decode, M <= 32; the kernels leave it zeroed) followed by the split-K slabs
- * or, for M >= 2048, the unpacked int8 weights of the prefill GEMM (rewritten every call).  One
+ * (decode, and prefill at 32 < M < 2048 when its 128 x 128 tiles are too few for the chip) or,
+ * for M >= 2048, the unpacked int8 weights of the prefill GEMM (rewritten every call).  One
  * buffer of the largest size may serve every shape on one stream.  Prefill without a workspace
- * (or a smaller one) still runs, with the weights unpacked per workgroup (bit-identical). */
+ * (or a smaller one) still runs: without split-K, and at M >= 2048 with the weights unpacked per
+ * workgroup (bit-identical). */
 size_t fq_gemm_workspace_bytes(int M, int N, int K);
 fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_t stream);
 

@@ -220,6 +220,8 @@ def test_gemm_deterministic(ops, dev):
     (1, 28672, 8192, 6), (8, 8192, 28672, 6), (16, 24576, 8192, 6),  # LLaMA-2-70B (BASELINE C4)
     # long K / many tiles per CU: the staging variants (activations, then scales, in the ring)
     (16, 8192, 28672, 6), (32, 28672, 8192, 8), (4, 8192, 65536, 6), (12, 16384, 16384, 8), (1, 57344, 8192, 6),
+    # 32 < M < 2048 with few 128 x 128 tiles: split-K prefill (fp32 slabs + reduce launch)
+    (64, 4096, 11008, 8), (100, 12288, 4096, 6), (33, 4096, 4096, 6),
 ])
 def test_gemm_full_size_sampled_columns(ops, dev, M, N, K, abits):
     """Full sizes: the whole GEMM runs on the GPU, the oracle checks a seeded sample of 96
@@ -474,7 +476,10 @@ def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     from flexq_amd import _lib
     L = _lib.load()
     assert L.fq_gemm_workspace_bytes(M, N, K) == 256 * 1024 + ((N + 15) // 16) * (K // 128) * 2048
-    assert L.fq_gemm_workspace_bytes(M // 2 - 1, N, K) == 0
+    # below the unpack threshold a workspace holds at most split-K slabs (fp32 [S][M][Npad])
+    Mh, npad = M // 2 - 1, (N + 15) // 16 * 16
+    wsh = L.fq_gemm_workspace_bytes(Mh, N, K)
+    assert wsh == 0 or (wsh - 256 * 1024) % (Mh * npad * 4) == 0
     g = torch.Generator(device=dev).manual_seed(M + N)
     xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
     wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
