@@ -1446,7 +1446,28 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
         const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
         const size_t lds_big = 2 * (size_t)(PB_ASTAGE + PB_BSTAGE);
         const bool xsf = M % PB_BM == 0;
-#define FQ_BIG(dbg, xf)                                                                                    \
+        // 256 x 256 or 128 x 128 tiles over the unpacked weights: the larger tile is ~13 % cheaper
+        // per MAC on a full chip, the smaller one fills it in finer steps (one WG per CU for 256 x
+        // 256, two for 128 x 128).  Take the 128 x 128 kernel when its last-round fill beats the
+        // 256 x 256 one's by more than that (tools/ab_pfm.sh, M = 2048 .. 8192 on the LLaMA-3-8B
+        // shapes: e.g. M = 2048, N = 4096: 128 WGs of 256 x 256 = half the CUs, 91 -> 69 us).
+        const double slots = device_cus();
+        const double fill_big = nbig / (ceil(nbig / slots) * slots), fill_128 = nwg / (ceil(nwg / (2 * slots)) * 2 * slots);
+        bool small_tiles = fill_big * 1.15 < fill_128;
+#ifdef FQ_DEV_ABLATION
+        if (const char *e = getenv("FQ_DEV_PF128")) small_tiles = atoi(e) != 0;  // development: force either
+#endif
+        if (small_tiles) {
+            if (acc_dbg)
+                hipLaunchKernelGGL((fq_gemm_prefill_kernel<true, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+                                   xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
+            else
+                hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+                                   xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
+            FQ_LAUNCH_CHECK();
+            return FQ_OK;
+        }
+#define FQ_BIG(dbg, xf)                                                                                  \
         hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
                            xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu)
         if (acc_dbg) {

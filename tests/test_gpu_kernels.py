@@ -467,7 +467,9 @@ def test_split_k_back_to_back_graph_replay(ops, dev, M, N, K):
         assert torch.equal(want[i].view(torch.int16), want[j].view(torch.int16))
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (2304, 1004, 1280), (4096, 4096, 4096)])
+# (2048, 1000) and (2304, 1004) run the 128 x 128 kernel over the unpacked weights (too few 256 x 256
+# tiles to fill the chip), (16384, 1004) and (4096, 4096) the 256 x 256 kernel (ragged N: per-element stores)
+@pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (2304, 1004, 1280), (16384, 1004, 1280), (4096, 4096, 4096)])
 def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     """Large M with a workspace: the weights are unpacked once (fq_unpack_w8_kernel) and the GEMM
     streams int8 operands (fq_gemm_prefill_kernel<U8>); without a workspace the GEMM unpacks per
@@ -477,7 +479,7 @@ def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     L = _lib.load()
     assert L.fq_gemm_workspace_bytes(M, N, K) == 256 * 1024 + ((N + 15) // 16) * (K // 128) * 2048
     # below the unpack threshold a workspace holds at most split-K slabs (fp32 [S][M][Npad])
-    Mh, npad = M // 2 - 1, (N + 15) // 16 * 16
+    Mh, npad = min(M // 2 - 1, 2047), (N + 15) // 16 * 16
     wsh = L.fq_gemm_workspace_bytes(Mh, N, K)
     assert wsh == 0 or (wsh - 256 * 1024) % (Mh * npad * 4) == 0
     g = torch.Generator(device=dev).manual_seed(M + N)
