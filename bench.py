@@ -447,7 +447,7 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
     Returns ms per token step for both and, with several ranks, the W6 step without its
     all-reduces."""
     from flexq_amd import convert
-    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear
+    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear, run_layers
     dev, tp, rank = ctx.dev, ctx.world, ctx.rank
     g = torch.Generator(device=dev).manual_seed(seed)  # the same full weights on every rank
     sq, sf = H ** -0.5, F ** -0.5
@@ -474,11 +474,8 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
         if tp > 1 and not ctx.staged:
             dist.all_reduce(t)
 
-    def step_w6(h, reduce=True):
-        for L in w6:
-            a = L.attention(h, reduce=reduce)
-            y = L.ffn(h, a, reduce=reduce)
-            h += y
+    def step_w6(h, reduce=True):  # each layer's last residual add fused into the next one's norm (FT)
+        run_layers(w6, h, reduce=reduce)
 
     def step_16(h):
         F_ = torch.nn.functional

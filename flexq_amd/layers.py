@@ -131,16 +131,33 @@ class FlexQDecoderLayer:
         ffn = FlexQFfn.from_dir(out_dir, layer, gamma_ffn, rank, device, eps, group)
         return cls(qkv, o, ffn, gamma_attn.to(device=device, dtype=torch.float16), attn_fn, eps)
 
-    def attention(self, h, reduce=True):
-        """h fp16 [M, H] (not modified) -> attention output [M, H] (this rank's partial sum when
-        reduce=False)."""
-        xq, xs = ops.rmsnorm_quantize(h, self.gamma_attn, self.qkv.abits, eps=self.eps)
+    def attention(self, h, reduce=True, pending=None):
+        """h fp16 [M, H] -> attention output [M, H] (this rank's partial sum when reduce=False).
+        h is not modified, unless `pending` (the previous layer's FFN output) is given: then
+        h += pending is fused into the pre-attention norm (FT's add-residual + norm kernel)."""
+        xq, xs = ops.rmsnorm_quantize(h, self.gamma_attn, self.qkv.abits, eps=self.eps, input=pending)
         ctx = self.attn_fn(self.qkv.from_codes(xq, xs))
         return self.o(ctx.contiguous(), reduce=reduce)
 
-    def __call__(self, h):
-        """h fp16 [M, H], updated in place to the layer output and returned."""
-        a = self.attention(h)
-        y = self.ffn(h, a)  # h += a (fused into the pre-FFN norm)
+    def __call__(self, h, pending=None, defer=False, reduce=True):
+        """h fp16 [M, H], updated in place to the layer output and returned.  With defer=True the
+        final residual add is left to the caller: the FFN output y is returned instead (h holds
+        the layer input + attention), to be passed as the next layer's `pending` -- one launch
+        less per layer, the same bits (the fused add is the same fp16 addition)."""
+        a = self.attention(h, reduce=reduce, pending=pending)
+        y = self.ffn(h, a, reduce=reduce)  # h += a (fused into the pre-FFN norm)
+        if defer:
+            return y
         h += y
         return h
+
+
+def run_layers(layers, h, reduce=True):
+    """Run decoder layers in order on h (in place), each layer's final residual add fused into the
+    next layer's pre-attention norm; returns h."""
+    pending = None
+    for L in layers:
+        pending = L(h, pending=pending, defer=True, reduce=reduce)
+    if pending is not None:
+        h += pending
+    return h

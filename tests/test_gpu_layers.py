@@ -139,6 +139,25 @@ def _decoder_weights():
     return {n: (torch.randn((H, H), generator=g) / H ** 0.5).half() for n in ("q", "k", "v", "o")}
 
 
+def test_run_layers_defers_residual_bit_identical(dev, weights, tmp_path):
+    """run_layers fuses each layer's final residual add into the next layer's pre-attention norm
+    (FT's add-residual + norm): the same bits as calling the layers one by one."""
+    from flexq_amd import convert
+    from flexq_amd.layers import FlexQDecoderLayer, run_layers
+    w, aw = weights, _decoder_weights()
+    ga = (1 + 0.1 * torch.randn(H, generator=torch.Generator().manual_seed(21))).half()
+    out = str(tmp_path / "tp1")
+    convert.convert_llama_safetensors(_ckpt(tmp_path, w, aw), out, tp_size=1, device=str(dev))
+    L = FlexQDecoderLayer.from_dir(out, 0, ga, w["gamma"], _attn_stand_in, device=dev)
+    for M in (1, 5):
+        x = torch.randn((M, H), generator=torch.Generator().manual_seed(22 + M)).half().to(dev)
+        h_ref = x.clone()
+        for _ in range(3):
+            L(h_ref)
+        h = run_layers([L, L, L], x.clone())
+        assert torch.equal(h.view(torch.int16), h_ref.view(torch.int16))
+
+
 @pytest.mark.parametrize("tp", [1, 2])
 def test_decoder_layer_tp(dev, weights, tmp_path, tp):
     """FlexQDecoderLayer (FT LlamaContextDecoder order) from converter files.  TP 1: the attention
