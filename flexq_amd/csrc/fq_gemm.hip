@@ -115,16 +115,18 @@ __device__ unsigned long long g_fq_stamps[1024 * 8];
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
-template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0>
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false>
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
-    const uint32_t *__restrict__ wpk, int M, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
-    float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir) {
+    const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
+    float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir,
+    int NCH) {
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
     // second serial round trip before the first DMA; tools/stamps.py).
-    asm volatile("" ::"s"(xq), "s"(xs), "s"(xh), "s"(abits), "s"(wpk), "s"(M), "s"(N), "s"(K), "s"(d), "s"(slabs),
+    asm volatile("" ::"s"(xq), "s"(xs), "s"(xh), "s"(abits), "s"(wpk), "s"(Mall), "s"(N), "s"(K), "s"(d), "s"(slabs),
                  "s"(tickets), "s"(S), "s"(IPW), "s"(RC), "s"(xwin), "s"(iq), "s"(ir), "s"(gridDim.x));
+    if (CH) asm volatile("" ::"s"(NCH));
     using C = DecodeCfg<MT, XS, SS>;
     constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
     static_assert(!FUSE || (XS == 0 && SS == 0), "fused quantization stages into LDS");
@@ -136,7 +138,20 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     // All index math is 32-bit and divides at most once per launch (64-bit or per-item divisions
     // cost microseconds of scalar code before the first DMA).  The grid is a multiple of S, so a
     // WG's k-split z is fixed and its items' tiles are t0, t0 + tstep, ...
-    const int bid = blockIdx.x, grid = gridDim.x;
+    // Row chunks (CH: NCH chunks of MT rows, 32 < M, S = 1): WG b serves rows [MT c, MT c + MT) of
+    // every tile it streams, c = b % NCH, as if it were WG b / NCH of a grid of gridDim.x / NCH on
+    // those rows; the x-scale stride stays the full M (ldx).  A separate instantiation: the index
+    // math below costs the one-chunk kernel ~0.15 us per launch when it is not compiled out.
+    const int c = CH ? (int)((unsigned)blockIdx.x % (unsigned)NCH) : 0;
+    const int bid = CH ? (int)((unsigned)blockIdx.x / (unsigned)NCH) : (int)blockIdx.x;
+    const int grid = CH ? (int)(gridDim.x / (unsigned)NCH) : (int)gridDim.x;
+    const int M = CH ? (Mall - MT * c < MT ? Mall - MT * c : MT) : Mall, ldx = Mall;
+    if (CH) {
+        xq += (size_t)MT * c * K;
+        xs += MT * c;
+        d += (size_t)MT * c * N;
+        if (DBG) acc_dbg += (size_t)MT * c * N * (K / FQ_GROUP);
+    }
     const int nit = iq + (bid < ir ? 1 : 0);  // items for this WG (>= 1): host-computed quotient
     const int z = S == 1 ? 0 : (unsigned)bid % (unsigned)S;
     const int t0 = S == 1 ? bid : (unsigned)bid / (unsigned)S, tstep = S == 1 ? grid : (unsigned)grid / (unsigned)S;
@@ -216,7 +231,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             if (!FUSE) {
                 for (int i0 = 0; i0 < ng; i0 += 64 / XSR) {  // x-scales: XSR per group, ushort per lane
                     const int i = i0 + lane / XSR, row = lane % XSR;
-                    __builtin_amdgcn_global_load_lds(xs + (long)(ga + (i < ng ? i : ng - 1)) * M + (row < M ? row : M - 1),
+                    __builtin_amdgcn_global_load_lds(xs + (long)(ga + (i < ng ? i : ng - 1)) * ldx + (row < M ? row : M - 1),
                                                      LDS_PTR(xs_st + i0 * XSR * 4), 2, 0, 0);
                 }
             }
@@ -251,7 +266,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             if (lane < 2)
                 __builtin_amdgcn_global_load_lds(wsb + ((long)t * G + g) * 16 + 8 * lane, LDS_PTR(dst + C::WS_OFF), 16, 0, 0);
             if (lane < XSR)
-                __builtin_amdgcn_global_load_lds(xs + (long)g * M + (lane < M ? lane : M - 1), LDS_PTR(dst + C::XS_OFF), 2, 0, 0);
+                __builtin_amdgcn_global_load_lds(xs + (long)g * ldx + (lane < M ? lane : M - 1), LDS_PTR(dst + C::XS_OFF), 2, 0, 0);
         }
     };
     // Order: first activation window -> ring block 0 -> staging -> ring blocks 1 .. D-1 (exactly
@@ -1101,6 +1116,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
 // =============================================================================================
 struct DecodePlan {
     int MT, S, grid, IPW, RC, XS, SS, xwin;  // xwin: fused fp16 window (0 = not fused)
+    int NCH;                                 // row chunks of MT rows (M > 32), else 1
     int NT;                                  // 16-column tiles
     int cost4;                               // modelled time, quarter-blocks per wave (see decode_plan)
     bool fits;
@@ -1119,6 +1135,7 @@ static int device_cus() {
 }
 
 static size_t decode_lds_bytes(const DecodePlan &p, int M, int N, int K) {
+    if (p.NCH > 1) M = p.MT;  // a WG holds one row chunk
     const int NW = decode_waves(p.MT);
     const int Gz = (K / FQ_GROUP + p.S - 1) / p.S;
     const int ngmax = (Gz + NW - 1) / NW;
@@ -1142,8 +1159,29 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused) {
     p.MT = M <= 4 ? 4 : (M <= 8 ? 8 : (M <= 16 ? 16 : 32));
     const int NT = (N + 15) / 16, G = K / FQ_GROUP;
     p.NT = NT;
+    p.NCH = 1;
     const int cus = device_cus();
     const int NW = decode_waves(p.MT);
+    if (M > 32) {  // row chunks of 32: every chunk streams the whole weight image, no k-split
+        p.NCH = (M + 31) / 32;
+        p.S = 1;
+        p.xwin = 0;
+        const int items = NT * p.NCH;
+        p.grid = (items < cus ? items : cus) / p.NCH * p.NCH;
+        if (p.grid < p.NCH) p.grid = p.NCH;
+        const int gw = p.grid / p.NCH;  // WGs per chunk
+        p.IPW = (NT + gw - 1) / gw;
+        p.cost4 = 4 * p.IPW * ((G + NW - 1) / NW) + kSplitQuantCost4;
+        const int modes[3][2] = {{0, 0}, {1, 0}, {1, 1}};
+        p.fits = false;
+        for (int m = 0; m < 3 && !p.fits; m++) {
+            p.XS = modes[m][0];
+            p.SS = modes[m][1];
+            for (p.RC = p.IPW; p.RC >= 1 && !p.fits; p.RC--) p.fits = decode_lds_bytes(p, M, N, K) <= kLdsMax;
+            if (p.fits) p.RC++;
+        }
+        return p;
+    }
     // k-split S minimises the modelled GEMM cost; S divides the grid so that z = blockIdx % S is
     // fixed per WG; ties keep the smaller S.  S (hence the summation order) is the same fused or
     // not, so fq_linear_w6ax gives the same bits whichever way it runs.
@@ -1248,12 +1286,25 @@ static int prefill_split(int M, int N, int K) {
 #endif
     return bs;
 }
+// 32 < M <= 64: the decode kernel in two row chunks of 32 (each chunk streams the weights, in one
+// launch) or the 128 x 128 prefill kernel (split-K when its tiles are few).  Measured
+// (tools/midm_sweep.py, M = 33 .. 256 on four LLaMA-2-7B shapes): the chunks win only while a chunk
+// is one round of tiles over short K -- 4096 x 4096 at M = 33 .. 64: 11.2-11.5 vs 14.3-16.5 us --
+// and lose from 12288 columns, K = 11008 or three chunks on (up to 2.5 x).
+static bool midm_decode(int M, int N, int K) {
+    if (M <= 32 || M > 256) return false;
+    bool use = M <= 64 && (N + 15) / 16 <= device_cus() && K <= 4096;
+#ifdef FQ_DEV_ABLATION
+    if (const char *e = getenv("FQ_DEV_MIDM")) use = atoi(e) != 0;  // development: force either
+#endif
+    return use;
+}
 static size_t prefill_slab_bytes(int M, int N, int S) { return (size_t)S * M * ((N + 15) / 16) * 16 * sizeof(float); }
 
 extern "C" size_t fq_gemm_workspace_bytes(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
     if (M >= PF_U8_MIN_M) return kTicketBytes + prefill_u8_bytes(N, K);  // tickets left untouched
-    if (M > 32) {
+    if (M > 32 && !midm_decode(M, N, K)) {
         const int S = prefill_split(M, N, K);
         return S > 1 ? kTicketBytes + prefill_slab_bytes(M, N, S) : 0;
     }
@@ -1295,20 +1346,21 @@ struct DecodeArgs {
     void *workspace;
 };
 
-template <int MT, int XS, int SS, bool FUSE, bool DBG>
+template <int MT, int XS, int SS, bool FUSE, bool DBG, bool CH = false>
 static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
     uint32_t *tickets = p.S > 1 ? (uint32_t *)a.workspace : nullptr;
     float *slabs = p.S > 1 ? (float *)((char *)a.workspace + kTicketBytes) : nullptr;
     const size_t lds = decode_lds_bytes(p, a.M, a.N, a.K);
     const dim3 grid(p.grid), block(decode_waves(MT) * 64);
 #ifdef FQ_DEV_ABLATION
-    if (!DBG && MT == 4 && XS == 0 && SS == 0) {  // (the fused and the unfused kernel)
+    if (!DBG && !CH && MT == 4 && XS == 0 && SS == 0) {  // (the fused and the unfused kernel)
         const int abl = dev_ablation();
 #define FQ_ABL(v)                                                                                           \
     if (abl == v) {                                                                                           \
         hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
                            a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
-                           slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / p.grid, p.NT * p.S % p.grid); \
+                           slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),              \
+                           p.NT * p.S % (p.grid / p.NCH), p.NCH);                                               \
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
@@ -1316,9 +1368,9 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 #undef FQ_ABL
     }
 #endif
-    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG>), grid, block, lds, stream, a.xq, a.xs, a.xh,
+    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH>), grid, block, lds, stream, a.xq, a.xs, a.xh,
                        a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S, p.IPW,
-                       p.RC, p.xwin, p.NT * p.S / p.grid, p.NT * p.S % p.grid);
+                       p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
@@ -1326,6 +1378,11 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 template <int MT, bool FUSE, bool DBG>
 static fq_status dispatch_modes(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
     if (FUSE) return launch_decode<MT, 0, 0, true, DBG>(p, a, stream);
+    if (MT == 32 && p.NCH > 1) {  // row chunks
+        if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG, true>(p, a, stream);
+        if (p.SS == 0) return launch_decode<MT, 1, 0, false, DBG, true>(p, a, stream);
+        return launch_decode<MT, 1, 1, false, DBG, true>(p, a, stream);
+    }
     if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG>(p, a, stream);
     if (p.SS == 0) return launch_decode<MT, 1, 0, false, DBG>(p, a, stream);
     return launch_decode<MT, 1, 1, false, DBG>(p, a, stream);
@@ -1382,7 +1439,7 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
     // The kernels are bit-width agnostic (int8 activations, values bounded by abits); abits is
     // validated for API parity with FLEXQGEMMWrapper(X_BITS, W_BITS, SIGNED).
     hipStream_t s = (hipStream_t)stream;
-    if (M <= 32) {
+    if (M <= 32 || midm_decode(M, N, K)) {
         DecodePlan p = decode_plan(M, N, K, false);
         const size_t need = fq_gemm_workspace_bytes(M, N, K);
         if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;

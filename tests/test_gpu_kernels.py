@@ -184,7 +184,8 @@ def test_gemm_kat(ops, dev, M, N, K, abits):
     assert_gemm_close(d, ref, mag, f"gemm M={M} N={N} K={K} a{abits}")
 
 
-@pytest.mark.parametrize("M,N,K,abits", [(1, 4096, 4096, 6), (16, 4096, 11008, 8), (16, 11008, 4096, 6), (256, 1024, 4096, 8)])
+@pytest.mark.parametrize("M,N,K,abits", [(1, 4096, 4096, 6), (16, 4096, 11008, 8), (16, 11008, 4096, 6), (256, 1024, 4096, 8),
+                                         (48, 4096, 4096, 6), (64, 2048, 4096, 8)])  # (row-chunked decode)
 def test_gemm_model_like(ops, dev, M, N, K, abits):
     _, _, xq, wq, xs, ws = model_operands(M, N, K, abits, seed=M + N + K)
     d, acc = run_gemm(ops, dev, xq, xs, wq, ws, abits)
