@@ -168,10 +168,38 @@ def time_graph(g, reps, stream):
 NORTH_STAR_SHAPES = [(24576, 8192), (8192, 8192), (28672, 8192), (8192, 28672)]  # test_flexq_kernel.sh:25-28
 
 
-def fp16_compare(shapes, M, abits, dev, reps=20):
+def int8_vendor_us(N, K, M, dev, g, s, reps):
+    """Context: the vendor int8 GEMM (torch._int_mm, int8 x int8 -> int32 on hipBLASLt; the
+    reference's W8A8 cuBLAS baseline, engine/test_cublas_kernel.cu:122-133) at the same N, K; M is
+    raised to the smallest size the op accepts when it rejects M.  Returns (us, M run)."""
+    copies = max(2, -(-768 * 2**20 // (N * K)))
+    w8 = [torch.randint(-128, 128, (N, K), dtype=torch.int8, device=dev, generator=g) for _ in range(copies)]
+    for Mi in (M, 17, 32):
+        if Mi < M:
+            continue
+        try:
+            x8 = torch.randint(-128, 128, (Mi, K), dtype=torch.int8, device=dev, generator=g)
+            with torch.cuda.stream(s):
+                torch._int_mm(x8, w8[0].t())
+            torch.cuda.synchronize()
+            break
+        except RuntimeError:
+            continue
+    else:
+        return None, None
+    gi = capture(lambda: [torch._int_mm(x8, w8[i % copies].t()) for i in range(reps)], s)
+    gi.replay()
+    torch.cuda.synchronize()
+    t = time_graph(gi, 5, s) / (5 * reps)
+    del gi, w8
+    return t, Mi
+
+
+def fp16_compare(shapes, M, abits, dev, reps=20, int8=False):
     """North-star denominator: rocBLAS/hipBLASLt fp16 GEMM (torch F.linear, fp16 weights) vs the
     W6Ax linear at the same (M, N, K).  Each side replays a graph of `reps` launches rotating over
-    enough weight copies (>= 768 MB) that the 256 MB MALL cannot serve them."""
+    enough weight copies (>= 768 MB) that the 256 MB MALL cannot serve them.  int8: also the vendor
+    int8 GEMM (context only, int8_vendor_us)."""
     out = []
     g = torch.Generator(device=dev).manual_seed(7)
     s = torch.cuda.Stream(dev)
@@ -194,10 +222,16 @@ def fp16_compare(shapes, M, abits, dev, reps=20):
         torch.cuda.synchronize()
         t16 = time_graph(g16, 5, s) / (5 * reps)
         t6 = time_graph(g6, 5, s) / (5 * reps)
-        out.append({"N": N, "K": K, "M": M, "fp16_us": round(t16 * 1e6, 2), "w6_us": round(t6 * 1e6, 2),
-                    "speedup": round(t16 / t6, 3)})
+        row = {"N": N, "K": K, "M": M, "fp16_us": round(t16 * 1e6, 2), "w6_us": round(t6 * 1e6, 2),
+               "speedup": round(t16 / t6, 3)}
         del g16, g6, w16, wq
         torch.cuda.synchronize()
+        if int8:
+            ti, mi = int8_vendor_us(N, K, M, dev, g, s, reps)
+            if ti is not None:
+                row.update(int8_vendor_us=round(ti * 1e6, 2), int8_vendor_M=mi, speedup_vs_int8=round(ti / t6, 3))
+            torch.cuda.synchronize()
+        out.append(row)
     return out
 
 
@@ -739,13 +773,18 @@ def main():
         torch.cuda.empty_cache()
         shapes = sorted({(N, K) for (_, N, K, _) in lins})
         ab_cfg = max(ab for (_, _, _, ab) in lins)
-        cmp_cfg = fp16_compare(shapes, M, ab_cfg, dev, reps=20 if not prefill else 4)
+        cmp_cfg = fp16_compare(shapes, M, ab_cfg, dev, reps=20 if not prefill else 4, int8=True)
         geo = lambda rows: round(float(np.exp(np.mean([np.log(r["speedup"]) for r in rows]))), 3)  # noqa: E731
         res["vs_rocblas_fp16"] = {
             "what": f"W6A{ab_cfg} linear (quantize+GEMM, one launch where fused) vs torch F.linear fp16 "
-                    "(hipBLASLt/rocBLAS), same M,N,K, graph-timed",
+                    "(hipBLASLt/rocBLAS), same M,N,K, graph-timed; config shapes also vs the vendor int8 "
+                    "GEMM torch._int_mm (context only: int8 x int8 -> int32, no quantize or dequant, "
+                    "int8_vendor_M = the smallest M it accepts)",
             "config_shapes": cmp_cfg, "config_geomean_speedup": geo(cmp_cfg),
         }
+        i8 = [r["speedup_vs_int8"] for r in cmp_cfg if "speedup_vs_int8" in r]
+        if i8:
+            res["vs_rocblas_fp16"]["config_geomean_speedup_vs_int8"] = round(float(np.exp(np.mean(np.log(i8)))), 3)
         if not prefill:
             cmp_ns = {m: fp16_compare(NORTH_STAR_SHAPES, m, 6, dev) for m in (1, 2, 4, 8)}
             res["vs_rocblas_fp16"].update({
