@@ -48,6 +48,12 @@ def gather_columns(local, group=None, out=None):
     returns [P][M][N/P] (rank-major); for M = 1 that already is [N], otherwise one transpose."""
     world = dist.get_world_size(group)
     M, n = local.shape
+    if out is None:
+        out = torch.empty((M, world * n), dtype=local.dtype, device=local.device)
+    if M == 1 and out.is_contiguous() and not (local.is_cuda and dist.get_backend(group) == "gloo"):
+        # rank-major IS the column order: gather straight into the output (no copy launch)
+        dist.all_gather_into_tensor(out.view(-1), local.contiguous().view(-1), group=group)
+        return out
     flat = torch.empty((world * M * n,), dtype=local.dtype, device=local.device)
     if local.is_cuda and dist.get_backend(group) == "gloo":  # gloo: device tensors through the host
         host = torch.empty((world * M * n,), dtype=local.dtype)
@@ -56,8 +62,6 @@ def gather_columns(local, group=None, out=None):
     else:
         dist.all_gather_into_tensor(flat, local.contiguous().view(-1), group=group)
     full = flat.view(world, M, n)
-    if out is None:
-        out = torch.empty((M, world * n), dtype=local.dtype, device=local.device)
     if M == 1:
         out.view(-1).copy_(flat)
     else:
