@@ -31,7 +31,10 @@ def _worker(rank, world, port, M, N, K, q):
         assert torch.equal(w_p, w[lo:hi]) and torch.equal(ws_p, ws[:, lo:hi])
         local = x @ w_p.t()                    # stands in for this rank's linear output
         full = gather_columns(local)
-        q.put((rank, torch.allclose(full, x @ w.t(), atol=1e-5), tuple(full.shape)))
+        pre = torch.full((M, N), float("nan"))  # caller-owned output (M = 1: gathered in place)
+        got = gather_columns(local, out=pre)
+        ok = torch.allclose(full, x @ w.t(), atol=1e-5) and got is pre and torch.equal(pre, full)
+        q.put((rank, ok, tuple(full.shape)))
     finally:
         dist.destroy_process_group()
 
