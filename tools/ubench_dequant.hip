@@ -6,11 +6,14 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 
 template <int MODE, int W>  // 0: MFMA only, 1: 16x16x64 + dequant, 2: 32x32x32 + dequant
 __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float *sink) {
@@ -69,6 +72,34 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
                     o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
                     o[2] = fmaf((float)acc[2], __low2float(p23), o[2]);
                     o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
+                }
+            }
+        } else if (MODE == 8 || MODE == 9) {
+            // 8: the group sums on the bf16 MFMA (int8 codes and 4w weights are exact in bf16, a
+            // group's sum is exact in fp32): four 16x16x32 per 16x16x128 block, no v_cvt; then the
+            // fma_mix + pk_mul dequant.  9: the bf16 MFMAs alone.
+#pragma unroll
+            for (int mi = 0; mi < 4; mi++) {
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++) {
+                    v4f acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, b[ni][0]), __builtin_bit_cast(v8bf, a[mi][0]), v4f{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, b[ni][1]), __builtin_bit_cast(v8bf, a[mi][1]), acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, b[ni][0]), __builtin_bit_cast(v8bf, a[mi][1]), acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, b[ni][1]), __builtin_bit_cast(v8bf, a[mi][0]), acc, 0, 0, 0);
+                    float *o = out[mi][ni];
+                    if (MODE == 9) {
+                        o[0] += acc[0] * acc[3];
+                        continue;
+                    }
+                    const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+                    const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                    const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                    o[0] = fmaf(acc[0], __low2float(p01), o[0]);
+                    o[1] = fmaf(acc[1], __high2float(p01), o[1]);
+                    o[2] = fmaf(acc[2], __low2float(p23), o[2]);
+                    o[3] = fmaf(acc[3], __high2float(p23), o[3]);
                 }
             }
         } else if (MODE == 3 || MODE == 4 || MODE == 5) {  // 3: no pk_mul, 4: no cvt, 5: neither
@@ -236,6 +267,13 @@ static void run(const char *name) {
 }
 
 int main() {
+    run<9, 8>("bf16 16x16x32 mfma only");
+    run<8, 8>("bf16 16x16x32 + dequant");
+    run<1, 8>("16x16x64 + dequant");
+    run<9, 4>("bf16 16x16x32 mfma only");
+    run<8, 4>("bf16 16x16x32 + dequant");
+    run<1, 4>("16x16x64 + dequant");
+    if (getenv("UBD_BF16_ONLY")) return 0;
     run<6, 4>("16x16 pipelined");
     run<7, 4>("32x32 pipelined");
     run<6, 8>("16x16 pipelined");
