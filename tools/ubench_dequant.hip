@@ -74,6 +74,28 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
                     o[3] = fmaf((float)acc[3], __high2float(p23), o[3]);
                 }
             }
+        } else if (MODE == 10) {
+            // 10: int8 MFMA seeded with the bits of 1.5 * 2^23, so the accumulator reads as the fp32
+            // 12582912 + acc (exact for |acc| < 2^22); one scalar v_sub_f32 per output replaces the cvt
+#pragma unroll
+            for (int mi = 0; mi < 4; mi++) {
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++) {
+                    const int B = 0x4B400000;
+                    v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{B, B, B, B}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
+                    const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
+                    const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                    const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                    float *o = out[mi][ni];
+                    o[0] = fmaf(__int_as_float(acc[0]) - 12582912.0f, __low2float(p01), o[0]);
+                    o[1] = fmaf(__int_as_float(acc[1]) - 12582912.0f, __high2float(p01), o[1]);
+                    o[2] = fmaf(__int_as_float(acc[2]) - 12582912.0f, __low2float(p23), o[2]);
+                    o[3] = fmaf(__int_as_float(acc[3]) - 12582912.0f, __high2float(p23), o[3]);
+                }
+            }
         } else if (MODE == 8 || MODE == 9) {
             // 8: the group sums on the bf16 MFMA (int8 codes and 4w weights are exact in bf16, a
             // group's sum is exact in fp32): four 16x16x32 per 16x16x128 block, no v_cvt; then the
@@ -273,6 +295,8 @@ int main() {
     run<9, 4>("bf16 16x16x32 mfma only");
     run<8, 4>("bf16 16x16x32 + dequant");
     run<1, 4>("16x16x64 + dequant");
+    run<10, 8>("16x16x64 biased + sub");
+    run<10, 4>("16x16x64 biased + sub");
     if (getenv("UBD_BF16_ONLY")) return 0;
     run<6, 4>("16x16 pipelined");
     run<7, 4>("32x32 pipelined");
