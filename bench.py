@@ -70,6 +70,12 @@ def alg_bytes(M, N, K, abits, fused=True):
     return N * K * 6 // 8 + 2 * N * K // GROUP + act + 2 * M * N
 
 
+def alg_read_bytes(M, N, K, abits, fused=True):
+    """The read part of alg_bytes (everything but the 2*M*N fp16 output): what rocprofv3's
+    FETCH_SIZE (a read counter) is compared with."""
+    return alg_bytes(M, N, K, abits, fused) - 2 * M * N
+
+
 def launch_list(lins, merge):
     """The step's launches: (name, N, K, abits).  merge: gate and up, which read the same input,
     run as one linear over their concatenated weights (one image [2N, K]; output [gate | up])."""
@@ -344,15 +350,35 @@ def cpu_baseline(budget_s=15.0, lins=None, M=1):
                 })
 
 
+def visible_gpus():
+    """GPUs this process may use, counted WITHOUT touching the HIP runtime (which any HIP call,
+    and torch's device count when amdsmi is unusable, would initialise before the spawn): KFD
+    topology nodes with SIMDs, narrowed by the *_VISIBLE_DEVICES lists.  None if unknown."""
+    import glob
+    try:
+        n = 0
+        for prop in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            with open(prop) as f:
+                kv = dict(line.split() for line in f if len(line.split()) == 2)
+            n += int(kv.get("simd_count", "0")) > 0
+    except (OSError, ValueError):
+        return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([d for d in v.split(",") if d.strip() != ""]))
+    return n if n > 0 else None
+
+
 def spawn_ranks(a):
     """`bench.py --gpus N` outside torchrun: start N ranks as a child torchrun (one process per GPU,
     127.0.0.1 rendezvous) and return its exit code.  Runs before anything touches the GPU
-    (torch.cuda.device_count() does not initialise it on this image), and the child is a separate
+    (visible_gpus() reads the KFD topology, no HIP call), and the child is a separate
     process: nothing is exec'd over a process that has used the GPU."""
     import socket
     import subprocess
-    n_dev = torch.cuda.device_count()
-    if n_dev < a.gpus and not a.share_gpu:
+    n_dev = visible_gpus()
+    if n_dev is not None and n_dev < a.gpus and not a.share_gpu:
         print(f"[bench] --gpus {a.gpus} but only {n_dev} GPU(s) visible", file=sys.stderr)
         return 2
     with socket.socket() as s_:
@@ -622,6 +648,7 @@ def main():
         tok_s = M * a.steps / elapsed
         per_launch_s = r["per_launch_us"] / 1e6
         bytes_launch = r["alg_bytes_per_launch"]
+        read_launch = bytes_launch
         fused_all = r["fused_launches"]
         use_graph = r["graph"]
         finite = r["finite"]
@@ -639,6 +666,7 @@ def main():
         fused = {(N, K): ops.act_scratch_bytes(M, N, K) == 0 for (_, N, K, _) in launch_lins}
         fused_all = all(fused.values())
         bytes_launch = layers * sum(alg_bytes(M, N, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins) / n_lin
+        read_launch = layers * sum(alg_read_bytes(M, N, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins) / n_lin
         last = linears(stack)[-1][1]["out"]
         finite = bool(torch.isfinite(last.float()).all().item())
         if prefill:  # MFMA-bound: the dominant kernel is the prefill GEMM; time its launches alone
@@ -695,7 +723,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "traffic_over_alg": round(traffic / bytes_launch, 4) if traffic else None,
+            "traffic_over_alg": round(traffic / read_launch, 4) if traffic else None,
+            "traffic_vs": "algorithmic READ bytes per launch (FETCH_SIZE counts reads only)",
             "per_launch_us": round(per_launch_s * 1e6, 3),
             "alg_bytes_per_launch": int(bytes_launch),
             "fused_launches": fused_all,
@@ -709,6 +738,7 @@ def main():
     if prefill and tp == 1:
         ach = ops_launch / per_gemm_s / 1e12
         bytes_pf = int(layers * sum(alg_bytes(M, N, K, ab, False) for (_, N, K, ab) in launch_lins) / n_lin)
+        read_pf = int(layers * sum(alg_read_bytes(M, N, K, ab, False) for (_, N, K, ab) in launch_lins) / n_lin)
         res["roofline"] = {
             "kernel": "fq_gemm_prefill_big_kernel" if M >= 2048 else "fq_gemm_prefill_kernel",
             "bound": "mfma",
@@ -718,7 +748,8 @@ def main():
             "frac": round(ach / I8_MFMA_PEAK_TOPS, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "traffic_over_alg": round(traffic / bytes_pf, 4) if traffic else None,
+            "traffic_over_alg": round(traffic / read_pf, 4) if traffic else None,
+            "traffic_vs": "algorithmic READ bytes per GEMM launch (FETCH_SIZE counts reads only)",
             "per_launch_us": round(per_gemm_s * 1e6, 3),
             "alg_ops_per_launch": ops_launch,
             "alg_bytes_per_launch": bytes_pf,

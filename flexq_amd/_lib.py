@@ -14,6 +14,9 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libflexq_hip.so")
+# development A/B only (tools/ab_decode.sh): another build of the same library
+if os.environ.get("FLEXQ_AMD_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["FLEXQ_AMD_LIB"])
 
 FQ_OK = 0
 _STATUS = {1: "FQ_ERR_NULL", 2: "FQ_ERR_SHAPE", 3: "FQ_ERR_BITS", 4: "FQ_ERR_WORKSPACE", 5: "FQ_ERR_HIP"}
@@ -38,6 +41,7 @@ SZ = ctypes.c_size_t
 # name -> (argtypes, restype)   -- mirrors include/flexq_hip.h
 _SIGS = {
     "fq_version": ([], ctypes.c_char_p),
+    "fq_abi_version": ([], I),
     "fq_status_string": ([I], ctypes.c_char_p),
     "fq_packed_w_bytes": ([I, I], SZ),
     "fq_gemm_workspace_bytes": ([I, I, I], SZ),

@@ -5,7 +5,8 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
                                  uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
                                  hipStream_t s, bool *launched);
 
-extern "C" const char *fq_version(void) { return "flexq_amd 0.1.0 (gfx950, int8-MFMA W6Ax)"; }
+extern "C" const char *fq_version(void) { return "flexq_amd 0.3.0 (gfx950, int8-MFMA W6Ax)"; }
+extern "C" int fq_abi_version(void) { return FQ_ABI_VERSION; }
 
 extern "C" const char *fq_status_string(fq_status s) {
     switch (s) {

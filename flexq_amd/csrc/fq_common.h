@@ -12,6 +12,9 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 #define FQ_GROUP 128
 #define FQ_WAVE 64
+// head of every GEMM workspace: the split-K tickets (one uint32 per 16-column tile, up to 65536
+// tiles), zeroed once by fq_workspace_init and left zeroed by the kernels
+constexpr size_t FQ_TICKET_BYTES = 256 * 1024;
 
 // ---- fp16 bit-pattern helpers (values travel as uint16_t through the C ABI) ----------------
 __device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }

@@ -154,7 +154,13 @@ class FlexQDecoderLayer:
 
 def run_layers(layers, h, reduce=True):
     """Run decoder layers in order on h (in place), each layer's final residual add fused into the
-    next layer's pre-attention norm; returns h."""
+    next layer's pre-attention norm; returns h.  reduce=False (no all-reduces) is a single-rank /
+    timing mode: with more than one rank the unreduced partial sums would feed the next layer's
+    norm, so it is rejected there."""
+    if not reduce and dist.is_initialized() and any(
+            L.o.row_parallel and dist.get_world_size(L.o.group) > 1 for L in layers):
+        raise ValueError("run_layers(reduce=False) is single-rank only: with more than one rank every "
+                         "layer's input must be the all-reduced sum")
     pending = None
     for L in layers:
         pending = L(h, pending=pending, defer=True, reduce=reduce)

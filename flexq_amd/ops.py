@@ -50,26 +50,37 @@ def gemm_workspace_bytes(M, N, K):
 
 
 _WS = {}
-_WS_RETIRED = []  # superseded workspaces: a HIP graph captured earlier may still address them
+_WS_CAPTURED = set()  # ids of workspaces a HIP graph capture has seen
+_WS_RETIRED = []  # superseded workspaces a captured graph may still address
 
 
 def workspace(device, nbytes, stream_handle):
     """Per-(device, stream) scratch for the split-K fix-up and the prefill weight unpack (zeroed
-    once, the ticket region kept zero by the kernels).  Growing it never frees the old buffer:
-    graphs captured before the growth bake its address into their launches (split-K tickets and
-    slabs, the unpack image), so it stays allocated -- and its tickets zero -- for the process."""
+    once, the ticket region kept zero by the kernels).  It grows geometrically (x1.5, 1 MiB
+    granules), so a rising sequence of shapes reallocates O(log) times.  A superseded buffer that a
+    graph capture has seen is kept for the process (the graph bakes its address into its launches:
+    split-K tickets and slabs, the unpack image); one no capture has seen is released."""
     if nbytes == 0:
         return None
     key = (device, stream_handle)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
-        nbytes = max(nbytes, 1 << 20)
-        if buf is not None:
+        old = buf.numel() if buf is not None else 0
+        nbytes = max(nbytes, old + old // 2, 1 << 20)
+        nbytes = (nbytes + (1 << 20) - 1) >> 20 << 20
+        if buf is not None and id(buf) in _WS_CAPTURED:
             _WS_RETIRED.append(buf)
         buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
         _lib.call("fq_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
         _WS[key] = buf
+    if torch.cuda.is_current_stream_capturing():
+        _WS_CAPTURED.add(id(buf))
     return buf
+
+
+def workspace_device_bytes():
+    """Bytes held by the workspaces (current and retired), for tests and diagnostics."""
+    return sum(b.numel() for b in _WS.values()) + sum(b.numel() for b in _WS_RETIRED)
 
 
 def reserve_workspace(device, shapes, stream=None):

@@ -21,12 +21,18 @@
  *     W_SCALE), into device memory the wrapper owns and frees in its destructor; FT's weights are
  *     loaded once and never rewritten.  set_weight_image(B, image) binds a caller-owned image
  *     instead (no allocation), forget_weight(B) drops a binding after B is rewritten.
- *   - The split-K tickets / slabs and the prefill unpack buffer live in a wrapper-owned, zeroed
- *     device workspace (grown, never shrunk, superseded buffers kept until destruction, so a
- *     captured graph never addresses freed memory).  flexq_gemm_workspace holds only the
- *     activation codes: workspace_bytes(M, N, K) bytes (the reference asks 6*M*maxK/8,
- *     LlamaV2ContextAttentionLayer.cc:793; here 2*M*K + M*K/64 + alignment, the first M*K of it
- *     left to the caller's pack() output exactly like the reference's half path, .cu:118).
+ *   - flexq_gemm_workspace is never required and never touched: FT's callers pass 6*M*maxK/8 bytes
+ *     (LlamaV2ContextAttentionLayer.cc:793, DecoderSelfAttentionLayer.cc:228) or nullptr and 0 (the
+ *     int path, FfnLayer.cc:371-401,521-561); both are accepted unchanged.  The activation codes
+ *     (int8, M*K bytes: more than the 6*M*K/8 bit planes the reference's pack() writes there), their
+ *     scales, the split-K tickets / slabs and the prefill unpack buffer live in ONE wrapper-owned
+ *     device scratch, zeroed on allocation and grown geometrically (x1.5, 1 MiB granules) so that a
+ *     rising sequence of shapes allocates O(log) times; superseded buffers are kept until
+ *     release_retired() or destruction, so a captured graph never addresses freed memory.
+ *   - gemm(const half* A ...) does not write x_scale.  The reference's half path writes the
+ *     duplicated x-scales there as a side effect of its internal pack() (.cu:118); this build keeps
+ *     them in its scratch (or, at decode sizes, never leaves the GEMM's LDS).  No FT caller reads
+ *     x_scale after the call; call pack() when the bit planes and x_scale are wanted.
  *   - C (bias), scale_inter and scale_out are unused, as in the reference (bias = true is rejected
  *     by FQBMMAOp::initialize, flexq_bmma_op.h:103-126).
  * Errors are printed as "[FlexQ][Error] ..." and the call returns, like the reference
@@ -51,16 +57,17 @@ class FLEXQGEMMWrapper {
     ~FLEXQGEMMWrapper() {
         for (auto &kv : images_)
             if (kv.second.owned) (void)hipFree(kv.second.ptr);
-        for (void *p : workspaces_) (void)hipFree(p);
+        if (scratch_) (void)hipFree(scratch_);
         release_retired();
     }
     FLEXQGEMMWrapper(const FLEXQGEMMWrapper &) = delete;
     FLEXQGEMMWrapper &operator=(const FLEXQGEMMWrapper &) = delete;
 
-    /* caller workspace (flexq_gemm_workspace) for gemm() at this shape */
+    /* caller workspace (flexq_gemm_workspace) gemm() needs: none.  Whatever the caller passes
+     * (FT: 6*M*maxK/8 bytes, or nullptr and 0) is accepted and left untouched. */
     static size_t workspace_bytes(int M, int N, int K) {
-        (void)N;
-        return 2 * align((size_t)M * K) + align((size_t)M * (K / 128) * 2);
+        (void)M, (void)N, (void)K;
+        return 0;
     }
 
     void pack(const half *in_data, int *packed_data, half *x_scale, int M, int K, int BIT, hipStream_t stream) {
@@ -72,36 +79,32 @@ class FLEXQGEMMWrapper {
     void gemm(const int M, const int N, const int K, const int *A, const int *B, const half *C, half *D,
               float *x_scale, const float *w_scale, const float *scale_inter, const float *scale_out, bool bias,
               char *flexq_gemm_workspace, size_t flexq_gemm_ws_bytes, hipStream_t stream = nullptr) {
-        (void)C, (void)scale_inter, (void)scale_out;
-        if (!check(M, N, K, bias, flexq_gemm_workspace, flexq_gemm_ws_bytes)) return;
+        (void)C, (void)scale_inter, (void)scale_out, (void)flexq_gemm_workspace, (void)flexq_gemm_ws_bytes;
+        if (!check(M, N, K, bias)) return;
         const void *img = image_for(B, reinterpret_cast<const uint16_t *>(w_scale), N, K, stream);
         if (!img) return;
-        int8_t *xq = reinterpret_cast<int8_t *>(flexq_gemm_workspace + align((size_t)M * K));
-        uint16_t *xs = reinterpret_cast<uint16_t *>(flexq_gemm_workspace + 2 * align((size_t)M * K));
-        if (!report(fq_import_ref_x(A, reinterpret_cast<const uint16_t *>(x_scale), M, K, x_bits_, xq, xs,
+        Scratch sc;
+        if (!scratch(M, N, K, stream, &sc)) return;
+        if (!report(fq_import_ref_x(A, reinterpret_cast<const uint16_t *>(x_scale), M, K, x_bits_, sc.xq, sc.xs,
                                     (fq_stream_t)stream),
                     "gemm: activation import"))
             return;
-        void *ws = gemm_workspace(M, N, K, stream);
-        if (!ws && fq_gemm_workspace_bytes(M, N, K)) return;
-        report(fq_gemm_w6ax(xq, xs, img, M, N, K, x_bits_, reinterpret_cast<uint16_t *>(D), nullptr, ws,
-                            ws_bytes_, (fq_stream_t)stream),
+        report(fq_gemm_w6ax(sc.xq, sc.xs, img, M, N, K, x_bits_, reinterpret_cast<uint16_t *>(D), nullptr, sc.ws,
+                            sc.ws_bytes, (fq_stream_t)stream),
                "gemm");
     }
 
     void gemm(const int M, const int N, const int K, const half *A, const int *B, const half *C, half *D,
               float *x_scale, const float *w_scale, const float *scale_inter, const float *scale_out, bool bias,
               char *flexq_gemm_workspace, size_t flexq_gemm_ws_bytes, hipStream_t stream = nullptr) {
-        (void)C, (void)x_scale, (void)scale_inter, (void)scale_out;
-        if (!check(M, N, K, bias, flexq_gemm_workspace, flexq_gemm_ws_bytes)) return;
+        (void)C, (void)x_scale, (void)scale_inter, (void)scale_out, (void)flexq_gemm_workspace, (void)flexq_gemm_ws_bytes;
+        if (!check(M, N, K, bias)) return;
         const void *img = image_for(B, reinterpret_cast<const uint16_t *>(w_scale), N, K, stream);
         if (!img) return;
-        int8_t *xq = reinterpret_cast<int8_t *>(flexq_gemm_workspace + align((size_t)M * K));
-        uint16_t *xs = reinterpret_cast<uint16_t *>(flexq_gemm_workspace + 2 * align((size_t)M * K));
-        void *ws = gemm_workspace(M, N, K, stream);
-        if (!ws && fq_gemm_workspace_bytes(M, N, K)) return;
+        Scratch sc;
+        if (!scratch(M, N, K, stream, &sc)) return;
         report(fq_linear_w6ax(reinterpret_cast<const uint16_t *>(A), M, N, K, x_bits_, img,
-                              reinterpret_cast<uint16_t *>(D), xq, xs, ws, ws_bytes_, (fq_stream_t)stream),
+                              reinterpret_cast<uint16_t *>(D), sc.xq, sc.xs, sc.ws, sc.ws_bytes, (fq_stream_t)stream),
                "gemm");
     }
 
@@ -110,7 +113,7 @@ class FLEXQGEMMWrapper {
     void forget_weight(const int *B) {
         auto it = images_.find(B);
         if (it == images_.end()) return;
-        if (it->second.owned) retired_images_.push_back(it->second.ptr);  // a graph may still read it
+        if (it->second.owned) retired_.push_back(it->second.ptr);  // a graph may still read it
         images_.erase(it);
     }
     fq_status status() const { return last_; }
@@ -128,12 +131,11 @@ class FLEXQGEMMWrapper {
         return s == FQ_OK;
     }
 
-    bool check(int M, int N, int K, bool bias, char *ws, size_t ws_bytes) {
+    bool check(int M, int N, int K, bool bias) {
         if (K < 128 || K % 128 != 0) return report(FQ_ERR_SHAPE, "unsupported K");  // .cu:43-46
         if (w_bits_ != 6 || (x_bits_ != 6 && x_bits_ != 8) || !signed_) return report(FQ_ERR_BITS, "unsupported w/a bits");
         if (M <= 0 || N <= 0) return report(FQ_ERR_SHAPE, "unsupported M/N");
         if (bias) return report(FQ_ERR_SHAPE, "bias is not supported (FQBMMAOp::initialize)");
-        if (!ws || ws_bytes < workspace_bytes(M, N, K)) return report(FQ_ERR_WORKSPACE, "flexq_gemm_workspace too small");
         return true;
     }
 
@@ -153,40 +155,61 @@ class FLEXQGEMMWrapper {
         return img;
     }
 
-    void *gemm_workspace(int M, int N, int K, hipStream_t stream) {
-        const size_t need = fq_gemm_workspace_bytes(M, N, K);
-        if (need <= ws_bytes_) return ws_;
-        void *p = nullptr;
-        if (hipMalloc(&p, need) != hipSuccess) {
-            report(FQ_ERR_HIP, "gemm workspace allocation");
-            return nullptr;
+    struct Scratch {
+        void *ws;
+        size_t ws_bytes;
+        int8_t *xq;
+        uint16_t *xs;
+    };
+    /* [GEMM workspace: at least the ticket region | xq int8 [M][K] | xs fp16 [K/128][M]]; the ticket
+     * region is always reserved at the head, so the codes of a shape without split-K never land on
+     * tickets a later split-K shape expects zeroed */
+    static size_t ws_region(int M, int N, int K) {
+        const size_t need = fq_gemm_workspace_bytes(M, N, K), tickets = 256 * 1024;
+        return align(need > tickets ? need : tickets);
+    }
+    bool scratch(int M, int N, int K, hipStream_t stream, Scratch *out) {
+        const size_t wsr = ws_region(M, N, K);
+        const size_t need = wsr + align((size_t)M * K) + align((size_t)M * (K / 128) * 2);
+        if (need > scratch_bytes_) {
+            size_t nb = scratch_bytes_ + scratch_bytes_ / 2;  // geometric growth
+            if (nb < need) nb = need;
+            nb = (nb + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+            void *p = nullptr;
+            if (hipMalloc(&p, nb) != hipSuccess) return report(FQ_ERR_HIP, "scratch allocation");
+            if (!report(fq_workspace_init(p, nb, (fq_stream_t)stream), "scratch init")) {
+                (void)hipFree(p);
+                return false;
+            }
+            if (scratch_) retired_.push_back(scratch_);  // a captured graph may still address it
+            scratch_ = p;
+            scratch_bytes_ = nb;
         }
-        if (!report(fq_workspace_init(p, need, (fq_stream_t)stream), "gemm workspace init")) {
-            (void)hipFree(p);
-            return nullptr;
-        }
-        workspaces_.push_back(p);  // the old one stays allocated until destruction
-        ws_ = p;
-        ws_bytes_ = need;
-        return ws_;
+        char *base = static_cast<char *>(scratch_);
+        out->ws = base;
+        out->ws_bytes = wsr;
+        out->xq = reinterpret_cast<int8_t *>(base + wsr);
+        out->xs = reinterpret_cast<uint16_t *>(base + wsr + align((size_t)M * K));
+        return true;
     }
 
     int x_bits_, w_bits_;
     bool signed_;
     fq_status last_ = FQ_OK;
     std::unordered_map<const int *, Image> images_;
-    std::vector<void *> retired_images_;
-    std::vector<void *> workspaces_;
-    void *ws_ = nullptr;
-    size_t ws_bytes_ = 0;
+    std::vector<void *> retired_;  // superseded scratch and forgotten images
+    void *scratch_ = nullptr;
+    size_t scratch_bytes_ = 0;
 
   public:
-    /* free images dropped by forget_weight() (once no captured graph reads them; the destructor
-     * frees them too) */
+    /* free superseded scratch buffers and images dropped by forget_weight() (once no captured
+     * graph reads them; the destructor frees them too) */
     void release_retired() {
-        for (void *p : retired_images_) (void)hipFree(p);
-        retired_images_.clear();
+        for (void *p : retired_) (void)hipFree(p);
+        retired_.clear();
     }
+    size_t scratch_bytes() const { return scratch_bytes_; }
+    size_t retired_count() const { return retired_.size(); }
 };
 
 }  // namespace flexq_amd

@@ -45,6 +45,13 @@ extern "C" {
 
 typedef struct ihipStream_t *fq_stream_t; /* == hipStream_t */
 
+/* ABI version.  3: fq_bmma_init takes reference bit-plane W + W_SCALE (the weight-image form is
+ * fq_bmma_init_image) and fq_bmma_state carries w_format / prepared; split-K prefill without its
+ * workspace returns FQ_ERR_WORKSPACE.  A caller built against another version should compare
+ * FQ_ABI_VERSION with fq_abi_version() at start-up. */
+#define FQ_ABI_VERSION 3
+int fq_abi_version(void);
+
 typedef int fq_status;
 #define FQ_OK 0
 #define FQ_ERR_NULL 1      /* a required pointer is NULL */
@@ -66,9 +73,10 @@ size_t fq_packed_w_bytes(int N, int K);
  * region (split-K decode, M <= 32; the kernels leave it zeroed) followed by the split-K slabs
  * (decode, and prefill at 32 < M < 2048 when its 128 x 128 tiles are too few for the chip) or,
  * for M >= 2048, the unpacked int8 weights of the prefill GEMM (rewritten every call).  One
- * buffer of the largest size may serve every shape on one stream.  Prefill without a workspace
- * (or a smaller one) still runs: without split-K, and at M >= 2048 with the weights unpacked per
- * workgroup (bit-identical). */
+ * buffer of the largest size may serve every shape on one stream.  A shape that needs split-K
+ * slabs returns FQ_ERR_WORKSPACE when the buffer is missing or short (the bits must not depend on
+ * the caller's buffer); at M >= 2048 a missing or short one only means the weights are unpacked
+ * per workgroup instead of once per call (bit-identical). */
 size_t fq_gemm_workspace_bytes(int M, int N, int K);
 fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_t stream);
 

@@ -1,16 +1,20 @@
-// test_wrapper.cpp -- drives include/flexq_gemm_wrapper.hpp (the FLEXQGEMMWrapper drop-in) the way
-// a FasterTransformer layer does (FfnLayer.cc:371-401): weights as reference bit planes + W_SCALE,
-// gemm(const half* A ...) for quantize + GEMM, and pack() + gemm(const int* A ...) for the
-// two-step form.  It writes its inputs and both outputs to <outdir> as raw little-endian files;
-// tests/test_gpu_wrapper.py checks them against the CPU oracle.  Test infrastructure only.
+// test_wrapper.cpp -- drives the two C++ drop-ins the way FasterTransformer's unchanged call sites
+// do: include/flexq_gemm_wrapper.hpp (FLEXQGEMMWrapper; FfnLayer.cc:371-401,521-561 call the int
+// path with a nullptr workspace, LlamaV2ContextAttentionLayer.cc:793 sizes its workspace
+// 6*M*maxK/8 bytes) and include/flexq_bmma_op.hpp (the named FQBMMA init/exec function pointers,
+// selected and called exactly as flexq_gemm_wrapper.cu:53-97 does).  It writes its inputs and the
+// outputs to <outdir> as raw little-endian files; tests/test_gpu_wrapper.py checks them against the
+// CPU oracle.  Test infrastructure only.
 //
 // usage: test_wrapper <outdir> <M> <N> <K> <abits> <seed>
+//        test_wrapper growth          (scratch growth over ascending M stays logarithmic)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
 
+#include "flexq_bmma_op.hpp"
 #include "flexq_gemm_wrapper.hpp"
 
 #define CK(x)                                                                         \
@@ -41,7 +45,48 @@ static void dump(const std::string &path, const std::vector<T> &v) {
     fclose(f);
 }
 
+// flexq_gemm_wrapper.cu:53-84: the reference's instance choice per (bits, M)
+static void pick(int abits, int M, FQBMMAInitFn_t *init_fn, FQBMMAExecFn_t *exec_fn) {
+    if (abits == 6) {
+        if (M == 1) *init_fn = FQBMMA_6x6xtrue_1x32x256_8x48x128_8x8x128_2_1_InitFn, *exec_fn = FQBMMA_6x6xtrue_1x32x256_8x48x128_8x8x128_2_1_ExecFn;
+        else if (M == 2) *init_fn = FQBMMA_6x6xtrue_2x32x512_16x48x128_8x8x128_2_1_InitFn, *exec_fn = FQBMMA_6x6xtrue_2x32x512_16x48x128_8x8x128_2_1_ExecFn;
+        else if (M == 4) *init_fn = FQBMMA_6x6xtrue_4x32x512_24x48x128_8x8x128_2_1_InitFn, *exec_fn = FQBMMA_6x6xtrue_4x32x512_24x48x128_8x8x128_2_1_ExecFn;
+        else *init_fn = FQBMMA_6x6xtrue_8x16x256_48x48x128_8x8x128_4_1_InitFn, *exec_fn = FQBMMA_6x6xtrue_8x16x256_48x48x128_8x8x128_4_1_ExecFn;
+    } else {
+        if (M == 1) *init_fn = FQBMMA_8x6xtrue_1x32x256_8x48x128_8x8x128_4_1_InitFn, *exec_fn = FQBMMA_8x6xtrue_1x32x256_8x48x128_8x8x128_4_1_ExecFn;
+        else if (M == 2) *init_fn = FQBMMA_8x6xtrue_2x32x256_16x48x128_8x8x128_4_1_InitFn, *exec_fn = FQBMMA_8x6xtrue_2x32x256_16x48x128_8x8x128_4_1_ExecFn;
+        else if (M == 4) *init_fn = FQBMMA_8x6xtrue_4x64x256_32x48x128_8x8x128_4_1_InitFn, *exec_fn = FQBMMA_8x6xtrue_4x64x256_32x48x128_8x8x128_4_1_ExecFn;
+        else *init_fn = FQBMMA_8x6xtrue_8x64x384_64x48x128_8x8x128_2_1_InitFn, *exec_fn = FQBMMA_8x6xtrue_8x64x384_64x48x128_8x8x128_2_1_ExecFn;
+    }
+}
+
+// a rising sequence of shapes must not leave one superseded scratch per new maximum
+static int growth() {
+    const int N = 4096, K = 4096;
+    __half *dx, *dd, *dws;
+    int32_t *dwp;
+    CK(hipMalloc(&dx, (size_t)2048 * K * 2));
+    CK(hipMalloc(&dd, (size_t)2048 * N * 2));
+    CK(hipMalloc(&dws, (size_t)(K / 128) * N * 2));
+    CK(hipMalloc(&dwp, (size_t)6 * N * (K / 32) * 4));
+    CK(hipMemset(dx, 0, (size_t)2048 * K * 2));
+    CK(hipMemset(dws, 0, (size_t)(K / 128) * N * 2));
+    CK(hipMemset(dwp, 0, (size_t)6 * N * (K / 32) * 4));
+    flexq_amd::FLEXQGEMMWrapper w(6, 6, true);
+    int calls = 0;
+    for (int M = 1; M <= 2048; M += 1 + M / 8, calls++) {
+        w.gemm(M, N, K, dx, dwp, nullptr, dd, nullptr, reinterpret_cast<const float *>(dws), nullptr, nullptr, false,
+               nullptr, 0, nullptr);
+        if (w.status() != FQ_OK) return 10;
+    }
+    CK(hipDeviceSynchronize());
+    printf("growth calls=%d scratch_bytes=%zu retired=%zu\n", calls, w.scratch_bytes(), w.retired_count());
+    for (void *p : {(void *)dx, (void *)dd, (void *)dws, (void *)dwp}) CK(hipFree(p));
+    return w.retired_count() <= 16 ? 0 : 11;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 2 && std::string(argv[1]) == "growth") return growth();
     if (argc != 7) {
         fprintf(stderr, "usage: %s outdir M N K abits seed\n", argv[0]);
         return 2;
@@ -64,16 +109,18 @@ int main(int argc, char **argv) {
 
     hipStream_t s;
     CK(hipStreamCreate(&s));
-    __half *dx, *dws, *dd1, *dd2, *dxs;
+    __half *dx, *dws, *dd1, *dd2, *dd3, *dxs;
     int32_t *dwraw, *dwp, *dxp;
     char *dwork;
     const size_t wpb = (size_t)6 * N * (K / 32) * 4, xpb = (size_t)abits * M * (K / 32) * 4;
     const size_t xsdup = (size_t)(K / 128) * 2 * ((M + 3) / 4 * 4) * 2;
-    const size_t work = flexq_amd::FLEXQGEMMWrapper::workspace_bytes(M, N, K);
+    // the caller workspace exactly as FT sizes it (LlamaV2ContextAttentionLayer.cc:793)
+    const size_t work = (size_t)6 * M * K / 8;
     CK(hipMalloc(&dx, x.size() * 2));
     CK(hipMalloc(&dws, ws.size() * 2));
     CK(hipMalloc(&dd1, (size_t)M * N * 2));
     CK(hipMalloc(&dd2, (size_t)M * N * 2));
+    CK(hipMalloc(&dd3, (size_t)M * N * 2));
     CK(hipMalloc(&dxs, xsdup));
     CK(hipMalloc(&dwraw, wraw.size() * 4));
     CK(hipMalloc(&dwp, wpb));
@@ -87,35 +134,55 @@ int main(int argc, char **argv) {
     if (fq_ref_bit_packing(dwraw, dwp, N, K, 6, (fq_stream_t)s) != FQ_OK) return 3;
 
     flexq_amd::FLEXQGEMMWrapper w(abits, 6, true);
-    // 1. gemm(const half* A ...): quantize + GEMM (one launch at decode sizes)
+    // 1. gemm(const half* A ...) with FT's 6*M*maxK/8 workspace: quantize + GEMM (one launch at
+    //    decode sizes); the workspace is accepted and left untouched
     w.gemm(M, N, K, dx, dwp, nullptr, dd1, reinterpret_cast<float *>(dxs), reinterpret_cast<const float *>(dws),
            nullptr, nullptr, false, dwork, work, s);
     if (w.status() != FQ_OK) return 4;
-    // 2. pack() into the workspace's head, then gemm(const int* A ...), as the reference's half
-    //    path does internally (flexq_gemm_wrapper.cu:99-122)
+    // 2. pack() into a bit-plane buffer, then gemm(const int* A ...) with a nullptr workspace, as
+    //    FfnLayer.cc:371-401 calls it
     w.pack(dx, dxp, dxs, M, K, abits, s);
     if (w.status() != FQ_OK) return 5;
     for (int rep = 0; rep < 2; rep++) {  // the second call reuses the imported weight image
         w.gemm(M, N, K, dxp, dwp, nullptr, dd2, reinterpret_cast<float *>(dxs), reinterpret_cast<const float *>(dws),
-               nullptr, nullptr, false, dwork, work, s);
+               nullptr, nullptr, false, nullptr, 0, s);
         if (w.status() != FQ_OK) return 6;
     }
-    // 3. the reference's rejections print and return
+    // 3. the FQBMMA function-pointer instances, called as flexq_gemm_wrapper.cu:53-97 does
+    FQBMMAInitFn_t init_fn;
+    FQBMMAExecFn_t exec_fn;
+    pick(abits, M, &init_fn, &exec_fn);
+    for (int rep = 0; rep < 2; rep++) {
+        FQBMMAOpState state = (*init_fn)(reinterpret_cast<const int *>(dxp), dwp, reinterpret_cast<half *>(dxs),
+                                         reinterpret_cast<const half *>(dws), M, N, K, dd3, 128, false);
+        if (!state.initSuccess) return 9;
+        (*exec_fn)(state, s);
+    }
+    // 4. the reference's rejections print and return (exactly two "[FlexQ][Error]" lines)
     w.gemm(M, N, 100, dx, dwp, nullptr, dd1, nullptr, nullptr, nullptr, nullptr, false, dwork, work, s);
     if (w.status() != FQ_ERR_SHAPE) return 7;
-    w.gemm(M, N, K, dx, dwp, nullptr, dd1, nullptr, nullptr, nullptr, nullptr, false, dwork, 16, s);
-    if (w.status() != FQ_ERR_WORKSPACE) return 8;
+    FQBMMAOpState bad = (*init_fn)(reinterpret_cast<const int *>(dxp), dwp, reinterpret_cast<half *>(dxs),
+                                   reinterpret_cast<const half *>(dws), M, N, K, dd3, 64, false);
+    if (bad.initSuccess) return 8;
     CK(hipStreamSynchronize(s));
+    {  // the caller's workspace was never written
+        std::vector<unsigned char> hw(work);
+        CK(hipMemcpy(hw.data(), dwork, work, hipMemcpyDeviceToHost));
+        for (unsigned char c : hw)
+            if (c != 0xA5) return 12;
+    }
 
-    std::vector<__half> d1((size_t)M * N), d2((size_t)M * N);
+    std::vector<__half> d1((size_t)M * N), d2((size_t)M * N), d3((size_t)M * N);
     CK(hipMemcpy(d1.data(), dd1, d1.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(d2.data(), dd2, d2.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(d3.data(), dd3, d3.size() * 2, hipMemcpyDeviceToHost));
     dump(out + "/x.f16", x);
     dump(out + "/wraw.i32", wraw);
     dump(out + "/ws.f16", ws);
     dump(out + "/d_half.f16", d1);
     dump(out + "/d_int.f16", d2);
-    for (void *p : {(void *)dx, (void *)dws, (void *)dd1, (void *)dd2, (void *)dxs, (void *)dwraw, (void *)dwp,
+    dump(out + "/d_bmma.f16", d3);
+    for (void *p : {(void *)dx, (void *)dws, (void *)dd1, (void *)dd2, (void *)dd3, (void *)dxs, (void *)dwraw, (void *)dwp,
                     (void *)dxp, (void *)dwork})
         CK(hipFree(p));
     CK(hipStreamDestroy(s));

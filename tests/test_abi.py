@@ -87,3 +87,27 @@ def test_wrappers_reject_cpu_tensors():
         ops.quantize_act(torch.zeros(1, 128, dtype=torch.float16), 6)
     with pytest.raises(ValueError, match="HIP device"):
         ops.pack_w6(torch.zeros(16, 128, dtype=torch.int8), torch.zeros(1, 16, dtype=torch.float16))
+
+
+def test_abi_version_matches_header():
+    from flexq_amd import _lib
+    m = re.search(r"#define FQ_ABI_VERSION (\d+)", open(HEADER).read())
+    assert m and _lib.load().fq_abi_version() == int(m.group(1))
+
+
+def test_fqbmma_instances_exported_with_reference_names():
+    """include/flexq_bmma_op.hpp: the eight FQBMMA init/exec function pointers the reference's
+    FLEXQGEMMWrapper names (flexq_gemm_wrapper.cu:53-84) are data symbols of the library, under the
+    reference's FQ_NAME_FUN spelling (common/base.h:286-289), so its wrapper links unchanged."""
+    from flexq_amd import _lib
+    hpp = open(os.path.join(ROOT, "include", "flexq_bmma_op.hpp")).read()
+    names = re.findall(r"FQ_AMD_DECL_INSTANCE\((FQBMMA_\w+)\)", hpp)
+    assert len(names) == 8
+    for n in names:  # <X_BITS>x<W_BITS>xtrue_<BLOCK>_<WARP>_<MMA>_<NSTAGE>_<STRIDE>
+        assert re.fullmatch(r"FQBMMA_[68]x6xtrue_\d+x\d+x\d+_\d+x\d+x\d+_8x8x128_\d_1", n), n
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    data = set(re.findall(r"\b[DdBb]\s+(FQBMMA_\w+)", nm.stdout))
+    for n in names:
+        assert {n + "_InitFn", n + "_ExecFn"} <= data, n
+    funcs = set(re.findall(r"\bT\s+(fq_bmma_op_\w+)", nm.stdout))
+    assert {"fq_bmma_op_forget_weight", "fq_bmma_op_device_bytes"} <= funcs

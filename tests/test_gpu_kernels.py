@@ -468,6 +468,47 @@ def test_split_k_back_to_back_graph_replay(ops, dev, M, N, K):
         assert torch.equal(want[i].view(torch.int16), want[j].view(torch.int16))
 
 
+def test_split_k_handoff_under_uneven_load(ops, dev):
+    """MI355X_MICROARCH.md "Test every hand-off under UNEVEN load, consumer L1-warm, checking every
+    word": the split-K decode hand-off (write-through slabs, agent-scope ticket, last arriver sums
+    with sc1 loads) runs while a second stream streams 1 GiB copies beside it, so its workgroups land
+    on CUs that are busy to different degrees and arrive unevenly; each launch reuses the tickets and
+    slabs of the one before it (the consumer CUs' caches warm with the previous launch's lines).
+    Every output word of 3 x 64 launches equals the quiet-GPU result."""
+    from flexq_amd import _lib
+    L = _lib.load()
+    cases = [(1, 512, 8192), (4, 1024, 28672), (16, 2048, 28672)]
+    g = torch.Generator(device=dev).manual_seed(17)
+    data = []
+    for (M, N, K) in cases:
+        assert L.fq_gemm_workspace_bytes(M, N, K) > 0  # the plan splits K
+        x = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+        pk = ops.pack_w6(torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g),
+                         (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half())
+        data.append((M, N, K, x, pk))
+    main = torch.cuda.Stream(dev)
+    with torch.cuda.stream(main):
+        want = [ops.linear_w6ax(x, pk, N, 6) for (M, N, K, x, pk) in data]
+    torch.cuda.synchronize()
+    R = 64
+    src = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    side = torch.cuda.Stream(dev)
+    outs = [[torch.full((M, N), -1.0, dtype=torch.float16, device=dev) for _ in range(R)] for (M, N, K, x, pk) in data]
+    with torch.cuda.stream(side):
+        for _ in range(6):
+            dst.copy_(src)
+    with torch.cuda.stream(main):
+        for i in range(R):
+            for c, (M, N, K, x, pk) in enumerate(data):
+                ops.linear_w6ax(x, pk, N, 6, out=outs[c][i])
+    torch.cuda.synchronize()
+    for c in range(len(data)):
+        for i in range(R):
+            assert torch.equal(outs[c][i].view(torch.int16), want[c].view(torch.int16)), f"case {c} launch {i}"
+    del src, dst
+
+
 # (2048, 1000) and (2304, 1004) run the 128 x 128 kernel over the unpacked weights (too few 256 x 256
 # tiles to fill the chip), (16384, 1004) and (4096, 4096) the 256 x 256 kernel (ragged N: per-element stores)
 @pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (2304, 1004, 1280), (16384, 1004, 1280), (4096, 4096, 4096)])
@@ -507,6 +548,11 @@ def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     (1000, 1000, 1280, 6, True),      # ragged M and N (partial WG tiles on both edges)
     (2048, 2048, 4096, 8, True),
     (16384, 4096, 4096, 8, False),    # LLaMA-3-8B prefill (BASELINE C5) o_proj shape
+    # C5's own wide and long shapes at C5's M, accumulators included (acc_dbg is [M, N, K/128]
+    # int32: 13-60 GB on the device, written by the debug kernel; the oracle sees the sample)
+    pytest.param(16384, 6144, 4096, 8, True, marks=pytest.mark.timeout(300)),    # qkv (GQA)
+    pytest.param(16384, 28672, 4096, 8, True, marks=pytest.mark.timeout(300)),   # gate_up merged
+    pytest.param(16384, 4096, 14336, 8, True, marks=pytest.mark.timeout(300)),   # down_proj: 112 groups
 ])
 def test_gemm_prefill_sampled(ops, dev, M, N, K, abits, with_acc):
     """Prefill sizes: the whole GEMM on the GPU, the oracle on a seeded sample of rows x columns."""
@@ -531,3 +577,44 @@ def test_gemm_prefill_sampled(ops, dev, M, N, K, abits, with_acc):
         np.testing.assert_array_equal(host(acc.index_select(0, rows_t).index_select(1, cols_t)), acc_ref)
     assert_gemm_close(host(d.index_select(0, rows_t).index_select(1, cols_t)), ref, mag,
                       f"prefill M={M} N={N} K={K}")
+
+
+def test_workspace_growth_is_geometric(ops, dev):
+    """rising M values (split-K slabs grow with M) must not leave a superseded buffer per
+    new maximum: growth is x1.5 and a buffer no graph capture has seen is released."""
+    from flexq_amd import _lib
+    L = _lib.load()
+    N, K = 4096, 4096
+    s = torch.cuda.Stream(dev)
+    g = torch.Generator(device=dev).manual_seed(9)
+    pk = ops.pack_w6(torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g),
+                     (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half())
+    before = ops.workspace_device_bytes()
+    needs = []
+    with torch.cuda.stream(s):
+        for M in range(33, 1024, 29):
+            needs.append(L.fq_gemm_workspace_bytes(M, N, K))
+            x = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+            ops.linear_w6ax(x, pk, N, 6)
+    torch.cuda.synchronize()
+    held = ops.workspace_device_bytes() - before
+    assert max(needs) > 0
+    assert held <= 2 * max(max(needs), 1 << 20), (held, max(needs))
+
+
+def test_prefill_split_k_without_workspace_is_an_error(ops, dev):
+    """a split-K prefill shape without its slabs returns FQ_ERR_WORKSPACE (as the split-K
+    decode does) instead of silently running S = 1, whose fp16 bits differ."""
+    import ctypes
+    from flexq_amd import _lib
+    L = _lib.load()
+    M, N, K = 96, 4096, 4096
+    assert L.fq_gemm_workspace_bytes(M, N, K) > 256 * 1024  # the plan splits K
+    xq = torch.zeros((M, K), dtype=torch.int8, device=dev)
+    xs = torch.zeros((K // 128, M), dtype=torch.float16, device=dev)
+    pk = torch.zeros(ops.packed_w_bytes(N, K), dtype=torch.uint8, device=dev)
+    d = torch.empty((M, N), dtype=torch.float16, device=dev)
+    P = ctypes.c_void_p
+    rc = L.fq_gemm_w6ax(P(xq.data_ptr()), P(xs.data_ptr()), P(pk.data_ptr()), M, N, K, 8, P(d.data_ptr()), None,
+                        None, 0, None)
+    assert rc == 4  # FQ_ERR_WORKSPACE
