@@ -573,27 +573,26 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_rs_kerne
     };
 
     // ---- the register ring: slot u holds block i (i % DR == u): 3 plane dwordx2 + the w-scale.
-    // Every slot is refilled unconditionally -- past the wave's last block with a re-read of its
-    // first one (L2-served, never consumed) -- so that no load sits under a branch: hipcc then waits
-    // exactly vmcnt(4 (DR - 1)) before each block (a conditional load makes its count conservative,
-    // down to vmcnt(0) in the loop).
+    // Every slot is refilled unconditionally -- past the wave's last block with a buffer load whose
+    // offset lies beyond the buffer's num_records, which returns zeros and never reaches memory --
+    // so that no load sits under a branch: hipcc then waits exactly vmcnt(4 (DR - 1)) before each
+    // block (a conditional load makes its count conservative, down to vmcnt(0) in the loop).
     v2u wr[DR][3];
     uint32_t sr[DR];
-    const char *wbytes = reinterpret_cast<const char *>(wpk) + lane * 8;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(wpk), 0, NT * G * FQ_BLOCK, 0x00020000);
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(wsb), 0, NT * G * 32, 0x00020000);
     // the w-scale as the dword holding the pair of columns (lane & 14, | 1): no zero-extension of a
     // loaded register (hipcc places one at the loop latch and waits for the load there)
-    const uint32_t *wsl = reinterpret_cast<const uint32_t *>(wsb + (lane & 14));
     const uint32_t wsel = (lane & 1) ? 0x03020302u : 0x01000100u;  // half2(ws, ws) of this lane's column
-    const int gdum = ga < G ? ga : G - 1;
     int rit = ng > 0 ? 0 : nit, rj = 0;  // (item, group) of the next block to issue
     auto issue = [&](v2u (&slot)[3], uint32_t &ss) {
         const bool real = rit < nit;  // wave-uniform
-        const int t = real ? item_tile(rit) : t0, g = real ? ga + rj : gdum;
-        const long blk = (long)t * G + g;
-        const char *src = wbytes + blk * FQ_BLOCK;
+        const uint32_t blk = real ? (uint32_t)(item_tile(rit) * G + ga + rj) : 0x80000000u / FQ_BLOCK;
+        const uint32_t wo = real ? blk * FQ_BLOCK : 0x80000000u, so = real ? blk * 32 : 0x80000000u;
 #pragma unroll
-        for (int r = 0; r < 3; r++) slot[r] = __builtin_nontemporal_load(reinterpret_cast<const v2u *>(src + r * 512));
-        ss = __builtin_nontemporal_load(wsl + blk * 8);
+        for (int r = 0; r < 3; r++)
+            slot[r] = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(wrs, wo + lane * 8 + r * 512, 0, FQ_W_AUX));
+        ss = __builtin_amdgcn_raw_buffer_load_b32(srs, so + (lane & 14) * 2, 0, FQ_W_AUX);
         if (real && ++rj == ng) {
             rj = 0;
             ++rit;
@@ -1650,7 +1649,8 @@ static fq_status launch_decode_rs(const DecodePlan &p, const DecodeArgs &a, hipS
 
 template <int MT, bool FUSE, bool DBG>
 static fq_status dispatch_modes(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
-    if (FUSE && MT == 4 && FQ_DEC_RS && decode_rs_lds_bytes(p, a.M, a.K) <= kLdsMax)
+    if (FUSE && MT == 4 && FQ_DEC_RS && decode_rs_lds_bytes(p, a.M, a.K) <= kLdsMax &&
+        (long)p.NT * (a.K / FQ_GROUP) * FQ_BLOCK < 0x80000000L)  // buffer offsets: 31 bits
         return launch_decode_rs<DBG>(p, a, stream);
     if (FUSE) return launch_decode<MT, 0, 0, true, DBG>(p, a, stream);
     if (MT == 32 && p.NCH > 1) {  // row chunks

@@ -81,7 +81,7 @@ def _worker(rank, world, port, q):
                 x = torch.from_numpy(act_input(M, K, seed=40 + M).astype(np.float16)).to(dev)
                 y = lin(x)
                 torch.cuda.synchronize()
-                q.put(((N, K, M, rank), y.cpu()))
+                q.put(((N, K, M, rank), y.cpu().numpy()))  # by value: the worker may exit first
             del img, lin
             torch.cuda.empty_cache()
     finally:
@@ -112,11 +112,11 @@ def test_llama2_70b_column_parallel_world8(dev):
             x = act_input(M, K, seed=40 + M).astype(np.float16)
             xq, xs = oracle.quantize_engine(x, 6)
             ref, _, mag = oracle.gemm(xq, xs, wq, ws)
-            y0 = res[(N, K, M, 0)].numpy()
+            y0 = res[(N, K, M, 0)]
             assert y0.shape == (M, N)
             assert_gemm_close(y0[:, cols], ref, mag, f"C4 {N}x{K} M={M} (8-way column-parallel)")
             for r in range(1, WORLD):
-                np.testing.assert_array_equal(res[(N, K, M, r)].numpy().view(np.uint16), y0.view(np.uint16))
+                np.testing.assert_array_equal(res[(N, K, M, r)].view(np.uint16), y0.view(np.uint16))
 
 
 def test_weight_hash_torch_numpy_agree():
