@@ -482,237 +482,6 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
 }
 
 // =============================================================================================
-// Register-streamed decode kernel (fused quantizer, M <= 4).  The same work split, weight image,
-// quantizer, MFMA core, dequant order and reductions as fq_gemm_decode_kernel<4, 0, 0, FUSE>, so
-// the outputs and accumulators are bit-identical; what differs is how the bytes arrive:
-//   * every lane loads its own 24 bytes of each fq6 block (the three planes' dwordx2 of its block
-//     lane: exactly its MFMA B operand) and the block's 16 w-scales straight into VGPRs -- a ring of
-//     DR blocks in registers, unrolled so every slot index is static -- instead of LDS-DMA into a
-//     ring of LDS slots read back by ds_read (cdna_hip_programming.md, "GEMV / M <= 16 decode
-//     weights: load straight to VGPRs, deep unroll, late vmcnt");
-//   * the fp16 activation chunks the wave quantizes come into VGPRs too (XC chunks of 4 (group,
-//     row) pairs per window), so the kernel issues no LDS-DMA at all and every vmcnt wait is the
-//     compiler's exact count (an LDS-DMA in flight makes hipcc wait vmcnt(0) at the next use of a
-//     register load);
-//   * LDS holds only the quantized codes and x-scales of the wave's groups and the reduction slots.
-// =============================================================================================
-#ifndef FQ_RS_DEPTH
-#define FQ_RS_DEPTH 4
-#endif
-
-__host__ __device__ inline int decode_rs_wave_lds(int MT, int ng, int M) {
-    return decode_xsst_bytes(ng, MT) + decode_xst_bytes(ng, M);
-}
-
-typedef __attribute__((address_space(3))) char lds_char;
-
-template <int MT, int XC, bool DBG, int DR>
-__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_rs_kernel(
-    const uint16_t *__restrict__ xh, int abits, const uint32_t *__restrict__ wpk, int M, int N, int K,
-    uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, float *__restrict__ slabs, uint32_t *__restrict__ tickets,
-    int S, int RC, int iq, int ir) {
-    constexpr int NW = decode_waves(MT), RG = MT <= 16 ? 1 : 2, XSR = 16 * RG;
-    static_assert(DR >= 2 && 4 * (DR - 1) + 4 * XC <= 63, "vmcnt range");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    lds_char *lsm = (lds_char *)smem;
-    const int G = K / FQ_GROUP, NT = (N + 15) / 16;
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int bid = blockIdx.x, grid = gridDim.x;
-    const int nit = iq + (bid < ir ? 1 : 0);
-    const int z = S == 1 ? 0 : (unsigned)bid % (unsigned)S;
-    const int t0 = S == 1 ? bid : (unsigned)bid / (unsigned)S, tstep = S == 1 ? grid : (unsigned)grid / (unsigned)S;
-    const int gz0 = S == 1 ? 0 : (unsigned)(z * G) / (unsigned)S;
-    const int gz1 = S == 1 ? G : (unsigned)((z + 1) * G) / (unsigned)S;
-    const int Gz = gz1 - gz0;
-    const int ngmax = (Gz + NW - 1) / NW;
-    const int ga = gz0 + (wid * Gz) / NW, gb = gz0 + ((wid + 1) * Gz) / NW;
-    const int ng = gb - ga;
-    const int n = ng * nit;
-    const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
-    (void)tstep;
-
-    const int wl = decode_rs_wave_lds(MT, ngmax, M);
-    lds_char *xs_st = lsm + wid * wl;                         // x-scales [ng][XSR] dwords
-    lds_char *x_st = xs_st + decode_xsst_bytes(ngmax, MT);    // codes [ng][M][128 B], swizzled
-    const int EM = M * 16;
-    float *red = reinterpret_cast<float *>(smem + NW * wl);   // [RC][NW][M*16]
-    int *flag = reinterpret_cast<int *>(red + RC * NW * EM);  // [IPW]
-    auto item_tile = [&](int it) { return t0 + it * tstep; };
-
-    // ---- activation window: XC chunks of 4 (group, row) pairs, 16 lanes x 16 B per pair
-    const int qsub = lane & 15;
-    const int R = ng * M;
-    v4i raw[XC];
-    auto x_load = [&](int r0) {
-#pragma unroll
-        for (int c = 0; c < XC; c++) {
-            int rg = r0 + 4 * c + (lane >> 4);
-            rg = rg < R ? rg : (R > 0 ? R - 1 : 0);  // (past the wave's pairs: a re-read, never stored)
-            const int j = M == 1 ? rg : rg / M, row = rg - j * M;
-            const int gg = ga + j < G ? ga + j : G - 1;
-            raw[c] = __builtin_nontemporal_load(
-                reinterpret_cast<const v4i *>(xh + (long)row * K + (long)gg * FQ_GROUP + qsub * 8));
-        }
-    };
-    auto x_quant = [&](int r0) {
-#pragma unroll
-        for (int c = 0; c < XC; c++) {
-            if (r0 + 4 * c < R) {  // wave-uniform
-                const int rg = r0 + 4 * c + (lane >> 4);
-                uint2 codes;
-                const uint16_t sh = quant_group16(make_uint4(raw[c][0], raw[c][1], raw[c][2], raw[c][3]), abits, codes);
-                if (rg < R) {
-                    const int j = M == 1 ? rg : rg / M, row = rg - j * M;
-                    *reinterpret_cast<__attribute__((address_space(3))) v2u *>(
-                        x_st + rg * 128 + xswz(row, qsub >> 1) + (qsub & 1) * 8) = v2u{codes.x, codes.y};
-                    if (qsub == 0) *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(xs_st + (j * XSR + row) * 4) = sh;
-                }
-            }
-        }
-    };
-
-    // ---- the register ring: slot u holds block i (i % DR == u): 3 plane dwordx2 + the w-scale.
-    // Every slot is refilled unconditionally -- past the wave's last block with a buffer load whose
-    // offset lies beyond the buffer's num_records, which returns zeros and never reaches memory --
-    // so that no load sits under a branch: hipcc then waits exactly vmcnt(4 (DR - 1)) before each
-    // block (a conditional load makes its count conservative, down to vmcnt(0) in the loop).
-    v2u wr[DR][3];
-    uint32_t sr[DR];
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(wpk), 0, NT * G * FQ_BLOCK, 0x00020000);
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(wsb), 0, NT * G * 32, 0x00020000);
-    // the w-scale as the dword holding the pair of columns (lane & 14, | 1): no zero-extension of a
-    // loaded register (hipcc places one at the loop latch and waits for the load there)
-    const uint32_t wsel = (lane & 1) ? 0x03020302u : 0x01000100u;  // half2(ws, ws) of this lane's column
-    int rit = ng > 0 ? 0 : nit, rj = 0;  // (item, group) of the next block to issue
-    auto issue = [&](v2u (&slot)[3], uint32_t &ss) {
-        const bool real = rit < nit;  // wave-uniform
-        const uint32_t blk = real ? (uint32_t)(item_tile(rit) * G + ga + rj) : 0x80000000u / FQ_BLOCK;
-        const uint32_t wo = real ? blk * FQ_BLOCK : 0x80000000u, so = real ? blk * 32 : 0x80000000u;
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-            slot[r] = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(wrs, wo + lane * 8 + r * 512, 0, FQ_W_AUX));
-        ss = __builtin_amdgcn_raw_buffer_load_b32(srs, so + (lane & 14) * 2, 0, FQ_W_AUX);
-        if (real && ++rj == ng) {
-            rj = 0;
-            ++rit;
-        }
-    };
-
-    // Order: the first activation window, then the ring's first DR blocks, then the quantizer.
-    x_load(0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < DR; u++) issue(wr[u], sr[u]);
-    __builtin_amdgcn_sched_barrier(0);
-    x_quant(0);
-    for (int r0 = 4 * XC; r0 < R; r0 += 4 * XC) {  // later windows (M > 1 or long K)
-        x_load(r0);
-        x_quant(r0);
-    }
-
-    int arow[RG];
-#pragma unroll
-    for (int rg = 0; rg < RG; rg++) arow[rg] = 16 * rg + (lane & 15) < M ? 16 * rg + (lane & 15) : M - 1;
-    const int Npad = NT * 16;
-    float cur[RG][4];
-#pragma unroll
-    for (int rg = 0; rg < RG; rg++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) cur[rg][r] = 0.f;
-    int it = 0, j = 0;  // (item, group) of the block being consumed
-
-    // one block out of slot u: unpack (frees the slot), refill it with block i + DR, MFMA + dequant,
-    // and at an item's last group its partial tile goes to reduction slot it % RC
-    auto consume = [&](int i, v2u (&slot)[3], uint32_t &ss) {
-        v4i b0 = unpack_fq6(slot[0][0], slot[1][0], slot[2][0]), b1 = unpack_fq6(slot[0][1], slot[1][1], slot[2][1]);
-        uint32_t w2u = __builtin_amdgcn_perm(ss, ss, wsel);  // half2(ws, ws)
-        // The slot's last reads happen here, before its refill is issued (the "memory" clobber keeps
-        // the compiler from hoisting the refill loads above them): the old and the new values of the
-        // slot never overlap, so they share registers and the loop carries the loads in flight
-        // without copies (a copy of an in-flight register would wait for its load).  Only values
-        // derived from the slot cross this point, never the slot registers themselves.
-        asm volatile("" : "+v"(b0), "+v"(b1), "+v"(w2u)::"memory");
-        issue(slot, ss);  // block i + DR (or a never-consumed re-read past the end)
-        __builtin_amdgcn_sched_barrier(0);
-        if (i >= n) return;  // wave-uniform; no memory instruction below depends on it
-        const int g = ga + j;
-        v4i a[RG][2];
-        v4i xd[RG];
-#pragma unroll
-        for (int rg = 0; rg < RG; rg++) {
-            const lds_char *xrow = x_st + (j * M + arow[rg]) * FQ_GROUP;
-#pragma unroll
-            for (int s = 0; s < 2; s++) a[rg][s] = *reinterpret_cast<const __attribute__((address_space(3))) v4i *>(xrow + xswz(arow[rg], 4 * s + (lane >> 4)));
-            xd[rg] = *reinterpret_cast<const __attribute__((address_space(3))) v4i *>(xs_st + 4 * (j * XSR + 16 * rg + 4 * (lane >> 4)));
-        }
-        const __half2 w2 = *reinterpret_cast<const __half2 *>(&w2u);
-        const int col = 16 * item_tile(it) + (lane & 15);
-#pragma unroll
-        for (int rg = 0; rg < RG; rg++) {
-            v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][0], b0, v4i{0, 0, 0, 0}, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][1], b1, acc, 0, 0, 0);
-            const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)xd[rg][1], (uint32_t)xd[rg][0], 0x05040100u);
-            const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)xd[rg][3], (uint32_t)xd[rg][2], 0x05040100u);
-            const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&x01), w2);  // fp16-rounded
-            const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&x23), w2);  // scale product
-            cur[rg][0] = fmaf((float)acc[0], __low2float(p01), cur[rg][0]);
-            cur[rg][1] = fmaf((float)acc[1], __high2float(p01), cur[rg][1]);
-            cur[rg][2] = fmaf((float)acc[2], __low2float(p23), cur[rg][2]);
-            cur[rg][3] = fmaf((float)acc[3], __high2float(p23), cur[rg][3]);
-            if (DBG) {
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = 16 * rg + 4 * (lane >> 4) + r;
-                    if (row < M && col < N) acc_dbg[((long)row * N + col) * G + g] = acc[r] >> 2;
-                }
-            }
-        }
-        if (++j == ng) {  // item end (wave-uniform)
-            const int rs = it % RC;
-#pragma unroll
-            for (int rg = 0; rg < RG; rg++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = 16 * rg + 4 * (lane >> 4) + r;
-                    if (row < M) red[(rs * NW + wid) * EM + row * 16 + (lane & 15)] = cur[rg][r] * 0.25f;
-                    cur[rg][r] = 0.f;
-                }
-            j = 0;
-            ++it;
-        }
-    };
-    for (int i0 = 0; i0 < n; i0 += DR) {
-#pragma unroll
-        for (int u = 0; u < DR; u++) consume(i0 + u, wr[u], sr[u]);
-    }
-
-    // ---- reductions: RC == IPW (host-checked), so once, after the whole stream; a wave with no
-    // groups (ng == 0) still joins the barriers and leaves zero partials
-    if (ng == 0) {
-        for (int k = 0; k < nit; k++)
-            for (int e = lane; e < EM; e += 64) red[(k * NW + wid) * EM + e] = 0.f;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    for (int e = threadIdx.x; e < nit * EM; e += NW * 64) {
-        const int k = e / EM, ee = e - k * EM;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; w++) v += red[(k * NW + w) * EM + ee];
-        const int row = ee >> 4, nn = 16 * item_tile(k) + (ee & 15);
-        if (S == 1) {
-            if (nn < N) d[(long)row * N + nn] = f2h(v);
-        } else {
-            __hip_atomic_store(&slabs[((long)z * M + row) * Npad + nn], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (S == 1) return;
-    decode_splitk_fixup<NW>(nit, S, M, N, Npad, EM, t0, tstep, slabs, tickets, d, flag);
-}
-
-// =============================================================================================
 // Prefill kernel (M > 32): int8-MFMA bound.  WG tile 128 (M) x 128 (N), 4 waves as 2 x 2, each
 // wave 64 x 64 = 4 x 4 tiles of 16x16; one k-step per 128-wide group; two WGs per CU, so that one
 // WG's barrier / LDS-latency chain overlaps the other's MFMAs.
@@ -1619,39 +1388,8 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
     return FQ_OK;
 }
 
-// Register-streamed fused decode (fq_gemm_decode_rs_kernel): M <= 4, one reduction after the stream.
-#ifndef FQ_DEC_RS
-#define FQ_DEC_RS 0
-#endif
-static size_t decode_rs_lds_bytes(const DecodePlan &p, int M, int K) {
-    const int NW = decode_waves(4), Gz = (K / FQ_GROUP + p.S - 1) / p.S, ngmax = (Gz + NW - 1) / NW;
-    return (size_t)NW * decode_rs_wave_lds(4, ngmax, M) + (size_t)p.IPW * NW * M * 16 * 4 + 4 * (size_t)p.IPW + 16;
-}
-template <bool DBG>
-static fq_status launch_decode_rs(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
-    uint32_t *tickets = p.S > 1 ? (uint32_t *)a.workspace : nullptr;
-    float *slabs = p.S > 1 ? (float *)((char *)a.workspace + kTicketBytes) : nullptr;
-    const int NW = decode_waves(4), Gz = (a.K / FQ_GROUP + p.S - 1) / p.S, ngmax = (Gz + NW - 1) / NW;
-    const int R = ngmax * a.M;  // (group, row) pairs of the busiest wave
-    const size_t lds = decode_rs_lds_bytes(p, a.M, a.K);
-    const int iq = p.NT * p.S / p.grid, ir = p.NT * p.S % p.grid;
-#define FQ_RS_LAUNCH(xc)                                                                                         \
-    hipLaunchKernelGGL((fq_gemm_decode_rs_kernel<4, xc, DBG, FQ_RS_DEPTH>), dim3(p.grid), dim3(NW * 64), lds, stream, \
-                       a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S,  \
-                       p.IPW, iq, ir)
-    if (R <= 4) FQ_RS_LAUNCH(1);
-    else if (R <= 8) FQ_RS_LAUNCH(2);
-    else FQ_RS_LAUNCH(4);
-#undef FQ_RS_LAUNCH
-    FQ_LAUNCH_CHECK();
-    return FQ_OK;
-}
-
 template <int MT, bool FUSE, bool DBG>
 static fq_status dispatch_modes(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
-    if (FUSE && MT == 4 && FQ_DEC_RS && decode_rs_lds_bytes(p, a.M, a.K) <= kLdsMax &&
-        (long)p.NT * (a.K / FQ_GROUP) * FQ_BLOCK < 0x80000000L)  // buffer offsets: 31 bits
-        return launch_decode_rs<DBG>(p, a, stream);
     if (FUSE) return launch_decode<MT, 0, 0, true, DBG>(p, a, stream);
     if (MT == 32 && p.NCH > 1) {  // row chunks
         if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG, true>(p, a, stream);
