@@ -93,7 +93,7 @@ def launch_list(lins, merge):
     return out
 
 
-def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
+def build_stack(cfg, rank, world, dev, merge=True, seed=1234, peer=False):
     """Random-init weights of the architecture and the step's data flow.  The linears form a real
     dependency chain, as in decoding: the input of each linear is the leading M*K values of the
     previous linear's output buffer (standing in for the out-of-scope attention / norm / SiLU
@@ -105,6 +105,7 @@ def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
     prev = torch.randn((M * lins[0][2],), dtype=torch.float16, device=dev, generator=g)  # the token(s)
     x_first = prev
     shared = {}  # prefill: one output buffer per linear kind, reused by every layer (stream-ordered)
+    gathers = {}  # peer-store gather (--gather peer): one PeerGather per full width, buffers alternate
     for _ in range(layers):
         L = {}
         for (name, N, K, abits) in launch_list(lins, merge):
@@ -127,6 +128,14 @@ def build_stack(cfg, rank, world, dev, merge=True, seed=1234):
             src = prev if name != "up" else L["gate"]["x"].view(-1)
             x = src[:M * K].view(M, K)
             L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full, x=x)
+            if peer and world > 1:
+                from flexq_amd.dist import PeerGather
+                if N not in gathers:
+                    gathers[N] = [PeerGather(M, N, device=dev), 0]
+                pg, uses = gathers[N]
+                full = pg.bufs[uses & 1].view(-1)
+                L[name].update(pg=pg, parity=uses & 1, full=full)
+                gathers[N][1] = uses + 1
             if name != "gate":
                 prev = (full if world > 1 else out).view(-1)
         stack.append(L)
@@ -143,6 +152,9 @@ def run_step(stack, M, world, group=None, gather=True, staged=False):
     one fused quantize+GEMM launch each), then one RCCL all-gather of the fp16 shard outputs per
     linear when world > 1 (staged: through host memory, for the gloo rehearsal of --share-gpu)."""
     for name, p in linears(stack):
+        if world > 1 and gather and "pg" in p:  # the all-gather fused into the GEMM epilogue
+            p["pg"].linear(p["x"], p["pk"], p["abits"], parity=p["parity"])
+            continue
         ops.linear_w6ax(p["x"], p["pk"], p["Nl"], p["abits"], out=p["out"])
         if world > 1 and gather:
             if staged:
@@ -466,15 +478,15 @@ class Ctx:
         return t / reps, t / (reps * launches)
 
 
-def measure_tp(ctx, cfg, merge, tp, steps, warmup):
+def measure_tp(ctx, cfg, merge, tp, steps, warmup, peer=False):
     """Column-parallel N-shard of every linear of cfg over tp ranks: each rank
     streams its N/tp rows, ONE all-gather per linear assembles the fp16 output.  Returns ms/step
     with and without the gathers (max over ranks), the per-rank roofline of the GEMM launches and
     the gather bytes."""
     layers, M, lins, _ = cfg
     launch_lins = launch_list(lins, merge)
-    stack = build_stack(cfg, ctx.rank, tp, ctx.dev, merge)
-    use_graph = not ctx.a.no_graph and not ctx.staged
+    stack = build_stack(cfg, ctx.rank, tp, ctx.dev, merge, peer=peer)
+    use_graph = not ctx.a.no_graph and (peer or not ctx.staged)
     replay = ctx.prepare(lambda: run_step(stack, M, tp, staged=ctx.staged), use_graph)
     elapsed, _ = ctx.timed(replay, steps, warmup)
     n_lin = layers * len(launch_lins)
@@ -604,6 +616,8 @@ def main():
                          "all-gather per linear, total work fixed (strong scaling, SURVEY.md §8(e)); "
                          "dp = independent replicas, one token stream per GPU (weak scaling)")
     ap.add_argument("--no-replicas", action="store_true", help="N > 1, tp: skip the replica (dp) measurement")
+    ap.add_argument("--no-peer", action="store_true",
+                    help="N > 1, tp: skip the peer-store gather variant (all-gather fused into the GEMM epilogue)")
     ap.add_argument("--no-c4", action="store_true",
                     help="N > 1: skip the LLaMA-2-70B column-parallel measurement (BASELINE config C4)")
     ap.add_argument("--no-layers", action="store_true",
@@ -774,6 +788,20 @@ def main():
                         "tok_per_s": round(world * M * a.steps / el_dp, 2),
                         "ms_per_step": round(el_dp / a.steps * 1e3, 4)}
             optional(res, "replicas", replicas)
+        if not a.no_peer and M <= 32:  # the all-gather fused into the GEMM epilogue
+            def tp_peer(c):
+                rp = measure_tp(ctx, c, merge, tp, max(2, a.steps // 2), max(1, a.warmup // 2), peer=True)
+                return {"what": "the same column-parallel stack, each all-gather fused into its GEMM's epilogue: "
+                                "peer stores into IPC-mapped gather buffers + one wait launch per linear "
+                                "(fq_linear_w6ax_gather / fq_gather_wait) instead of an RCCL all_gather",
+                        "value": round(rp["flops_step"] / (rp["ms_per_step"] / 1e3) / 1e12, 4),
+                        "unit": "TFLOPS-equiv", "tok_per_s": round(M * 1e3 / rp["ms_per_step"], 2),
+                        "ms_per_step": round(rp["ms_per_step"], 4),
+                        "gemm_only_ms_per_step": round(rp["gemm_only_ms_per_step"], 4),
+                        "finite": rp["finite"], "graph": rp["graph"]}
+            optional(res, "tp_peer_gather", lambda: tp_peer(cfg))
+            if not a.no_c4 and a.config != "llama2-70b-m1":
+                optional(res, "c4_llama2_70b_tp_peer_gather", lambda: tp_peer(CONFIGS["llama2-70b-m1"]))
         if not a.no_c4 and a.config != "llama2-70b-m1" and not prefill:
             def c4_tp():
                 c4 = CONFIGS["llama2-70b-m1"]

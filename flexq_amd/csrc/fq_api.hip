@@ -3,7 +3,10 @@
 
 fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
                                  uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
-                                 hipStream_t s, bool *launched);
+                                 hipStream_t s, bool *launched, const fq_gather *gat);
+fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
+                            int abits, uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
+                            fq_stream_t stream, const fq_gather *gat);
 
 extern "C" const char *fq_version(void) { return "flexq_amd 0.3.0 (gfx950, int8-MFMA W6Ax)"; }
 extern "C" int fq_abi_version(void) { return FQ_ABI_VERSION; }
@@ -30,13 +33,31 @@ extern "C" fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int 
     // decode sizes: one launch, the quantizer runs inside the GEMM's prologue (xq/xs untouched)
     bool launched = false;
     fq_status st = fq_decode_linear_fused(x, M, N, K, abits, w_packed, d, nullptr, workspace,
-                                          workspace_bytes, (hipStream_t)stream, &launched);
+                                          workspace_bytes, (hipStream_t)stream, &launched, nullptr);
     if (launched || st != FQ_OK) return st;
     if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
     st = fq_quantize_act(x, M, K, abits, xq_buf, xs_buf, stream);
     if (st != FQ_OK) return st;
     return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace,
                         workspace_bytes, stream);
+}
+
+extern "C" fq_status fq_linear_w6ax_gather(const uint16_t *x, int M, int N, int K, int abits,
+                                           const void *w_packed, const fq_gather *gather, int8_t *xq_buf,
+                                           uint16_t *xs_buf, void *workspace, size_t workspace_bytes,
+                                           fq_stream_t stream) {
+    if (!x || !w_packed || !gather) return FQ_ERR_NULL;
+    if (M <= 0 || M > 32 || N <= 0 || N % 16 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    bool launched = false;
+    fq_status st = fq_decode_linear_fused(x, M, N, K, abits, w_packed, nullptr, nullptr, workspace,
+                                          workspace_bytes, (hipStream_t)stream, &launched, gather);
+    if (launched || st != FQ_OK) return st;
+    if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
+    st = fq_quantize_act(x, M, K, abits, xq_buf, xs_buf, stream);
+    if (st != FQ_OK) return st;
+    return fq_gemm_w6ax_impl(xq_buf, xs_buf, w_packed, M, N, K, abits, nullptr, nullptr, workspace,
+                             workspace_bytes, stream, gather);
 }
 
 // ---- FQBMMAOpState-style interface (flexq_bmma_op.h:19-34,163-188) ---------------------------

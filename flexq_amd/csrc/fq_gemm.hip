@@ -112,6 +112,36 @@ __device__ unsigned long long g_fq_stamps[1024 * 8];
 #define FQ_STAMP(k)
 #endif
 
+// ---- peer-store gather (column-parallel decode, fq_linear_w6ax_gather): each rank stores its output
+// tiles straight into every rank's [M][ld] gather buffer (IPC-mapped device pointers; on an 8-GPU
+// node these are stores over xGMI) at column offset col0, so the all-gather is the GEMM epilogue.
+// Stores are system-scope write-through (sc0 sc1), 4 bytes = two adjacent columns each.  After the
+// last workgroup's ticket (every workgroup's stores drained first), it raises this rank's flag in
+// every rank's flag array to gen + 1; fq_gather_wait_kernel on each rank waits for all P flags.
+__device__ __forceinline__ void gather_store2(const fq_gather *__restrict__ gat, int P, int row, int col,
+                                              float v0, float v1) {
+    const uint32_t pk = (uint32_t)f2h(v0) | ((uint32_t)f2h(v1) << 16);
+    const long off = (long)row * gat->ld + gat->col0 + col;
+    for (int q = 0; q < P; q++)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(gat->out[q] + off), pk, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void gather_publish(const fq_gather *__restrict__ gat) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its peer stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(gat->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {  // the last workgroup: every store of this launch has drained
+            __hip_atomic_store(gat->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t val = __hip_atomic_load(gat->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the fence's own wait can be dropped)
+            for (int q = 0; q < gat->P; q++)
+                __hip_atomic_store(gat->flags[q] + gat->rank, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // ---- deferred split-K fix-up of the decode kernels.  Every item's partial tile went out as
 // write-through (sc1) slab stores; one drain, then one agent-scope ticket per item (taken in
 // parallel, one lane each), and the last arriver of a tile sums its S slabs in z order.
@@ -134,7 +164,7 @@ template <int NW>
 __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N, int Npad, int EM, int t0,
                                                     int tstep, float *__restrict__ slabs,
                                                     uint32_t *__restrict__ tickets, uint16_t *__restrict__ d,
-                                                    int *flag) {
+                                                    int *flag, const fq_gather *__restrict__ gat) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if ((int)threadIdx.x < nit) {
@@ -145,9 +175,22 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
         flag[threadIdx.x] = last;
     }
     __syncthreads();  // (the flag is read behind this barrier: the slab loads cannot move above it)
+    const int GP = gat ? gat->P : 0;  // (gather: two adjacent columns per thread, 4-byte stores)
     for (int it = 0; it < nit; it++) {
         if (!flag[it]) continue;  // workgroup-uniform
         const int t = t0 + it * tstep;
+        if (gat) {
+            for (int e = 2 * threadIdx.x; e < EM; e += 2 * NW * 64) {
+                const int row = e >> 4, nn = 16 * t + (e & 15);
+                float v0 = 0.f, v1 = 0.f;
+                for (int z0 = 0; z0 < S; z0++) {
+                    v0 += __hip_atomic_load(&slabs[((long)z0 * M + row) * Npad + nn], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v1 += __hip_atomic_load(&slabs[((long)z0 * M + row) * Npad + nn + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                gather_store2(gat, GP, row, nn, v0, v1);
+            }
+            continue;
+        }
         for (int e = threadIdx.x; e < EM; e += NW * 64) {
             const int row = e >> 4, nn = 16 * t + (e & 15);
             float v = 0.f;
@@ -175,7 +218,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
     float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir,
-    int NCH) {
+    int NCH, const fq_gather *__restrict__ gat) {
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
     // second serial round trip before the first DMA; tools/stamps.py).
@@ -456,6 +499,18 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
+            if (S == 1 && gat) {  // peer-store gather: two adjacent columns per thread
+                for (int e = 2 * threadIdx.x; e < (rs + 1) * EM; e += 2 * NW * 64) {
+                    const int k = e / EM, ee = e - k * EM;
+                    float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+                    for (int w = 0; w < NW; w++) {
+                        v0 += red[(k * NW + w) * EM + ee];
+                        v1 += red[(k * NW + w) * EM + ee + 1];
+                    }
+                    gather_store2(gat, gat->P, ee >> 4, 16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
+                }
+            } else
             for (int e = threadIdx.x; e < (rs + 1) * EM; e += NW * 64) {
                 const int k = e / EM, ee = e - k * EM;
                 float v = 0.f;
@@ -476,9 +531,31 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
         }
     }
     FQ_STAMP(3);
-    if (S == 1 || (ABL & 4)) return;
-    decode_splitk_fixup<NW>(nit, S, M, N, Npad, EM, t0, tstep, slabs, tickets, d, flag);
+    if (S > 1 && !(ABL & 4)) decode_splitk_fixup<NW>(nit, S, M, N, Npad, EM, t0, tstep, slabs, tickets, d, flag, gat);
     FQ_STAMP(4);
+    if (gat) gather_publish(gat);
+}
+
+// Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q
+// polls rank q's flag with system-scope loads, sleeping between polls), then acquire and advance
+// the generation.  Bounded: after ~4 s the error word is set and the kernel returns (results are
+// then undefined, never a hang).
+__global__ __launch_bounds__(64) void fq_gather_wait_kernel(const fq_gather *__restrict__ gat, uint32_t *__restrict__ err) {
+    const int lane = threadIdx.x;
+    const uint32_t target = __hip_atomic_load(gat->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const uint32_t *mine = gat->flags[gat->rank];
+    bool ok = lane >= gat->P;
+    for (int spin = 0; spin < (1 << 22); spin++) {  // ~4 s at ~1 us per poll
+        if (!ok) ok = __hip_atomic_load(mine + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        if (lane == 0 && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    if (lane == 0) __hip_atomic_store(gat->gen, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // =============================================================================================
@@ -1357,6 +1434,7 @@ struct DecodeArgs {
     uint16_t *d;
     int32_t *acc_dbg;
     void *workspace;
+    const fq_gather *gat;  // peer-store gather (device memory), or nullptr
 };
 
 template <int MT, int XS, int SS, bool FUSE, bool DBG, bool CH = false>
@@ -1373,7 +1451,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
                            a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
                            slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),              \
-                           p.NT * p.S % (p.grid / p.NCH), p.NCH);                                               \
+                           p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat);                                        \
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
@@ -1383,7 +1461,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 #endif
     hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH>), grid, block, lds, stream, a.xq, a.xs, a.xh,
                        a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S, p.IPW,
-                       p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH);
+                       p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
@@ -1431,32 +1509,42 @@ extern "C" size_t fq_linear_act_scratch_bytes(int M, int N, int K) {
 // One-launch decode linear (quantize + GEMM) when the staged plan fits; FQ_ERR_SHAPE otherwise.
 fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
                                  uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
-                                 hipStream_t s, bool *launched) {
+                                 hipStream_t s, bool *launched, const fq_gather *gat) {
     *launched = false;
     DecodePlan p;
     if (!decode_fuse(M, N, K, &p)) return FQ_OK;
     const size_t need = fq_gemm_workspace_bytes(M, N, K);
     if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
-    DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace};
+    DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace, gat};
     *launched = true;
     return acc_dbg ? dispatch_decode<true, true>(p, a, s) : dispatch_decode<true, false>(p, a, s);
 }
 
+fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
+                            int abits, uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
+                            fq_stream_t stream, const fq_gather *gat);
 extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N,
                                   int K, int abits, uint16_t *d, int32_t *acc_dbg, void *workspace,
                                   size_t workspace_bytes, fq_stream_t stream) {
-    if (!xq || !xs || !w_packed || !d) return FQ_ERR_NULL;
+    return fq_gemm_w6ax_impl(xq, xs, w_packed, M, N, K, abits, d, acc_dbg, workspace, workspace_bytes, stream, nullptr);
+}
+
+fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
+                            int abits, uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
+                            fq_stream_t stream, const fq_gather *gat) {
+    if (!xq || !xs || !w_packed || (!d && !gat)) return FQ_ERR_NULL;
+    if (gat && (M > 32 || N % 16)) return FQ_ERR_SHAPE;  // peer-store gather: decode sizes, whole tiles
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
     if ((size_t)((N + 15) / 16) > kTicketBytes / 4) return FQ_ERR_SHAPE;
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     // The kernels are bit-width agnostic (int8 activations, values bounded by abits); abits is
     // validated for API parity with FLEXQGEMMWrapper(X_BITS, W_BITS, SIGNED).
     hipStream_t s = (hipStream_t)stream;
-    if (M <= 32 || midm_decode(M, N, K)) {
+    if (M <= 32 || (!gat && midm_decode(M, N, K))) {
         DecodePlan p = decode_plan(M, N, K, false);
         const size_t need = fq_gemm_workspace_bytes(M, N, K);
         if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
-        DecodeArgs a = {xq, xs, nullptr, abits, w_packed, M, N, K, d, acc_dbg, workspace};
+        DecodeArgs a = {xq, xs, nullptr, abits, w_packed, M, N, K, d, acc_dbg, workspace, gat};
         return acc_dbg ? dispatch_decode<false, true>(p, a, s) : dispatch_decode<false, false>(p, a, s);
     }
     const int NT = (N + 15) / 16;
@@ -1570,5 +1658,12 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
                            (const float *)slabs, S, M, N, d);
         FQ_LAUNCH_CHECK();
     }
+    return FQ_OK;
+}
+
+extern "C" fq_status fq_gather_wait(const fq_gather *gather, uint32_t *err, fq_stream_t stream) {
+    if (!gather) return FQ_ERR_NULL;
+    hipLaunchKernelGGL(fq_gather_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, gather, err);
+    FQ_LAUNCH_CHECK();
     return FQ_OK;
 }

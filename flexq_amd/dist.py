@@ -135,3 +135,158 @@ class RowParallelW6Linear:
         if self.world > 1 and reduce:
             all_reduce_sum(part, self.group)
         return part
+
+
+# ------------------------------------------------------------------------- peer-store all-gather
+
+def _hip():
+    """The HIP runtime torch already loaded (IPC calls only; kernels go through libflexq_hip.so)."""
+    import ctypes
+    import ctypes.util
+    for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
+        try:
+            return ctypes.CDLL(name)
+        except OSError:
+            continue
+    raise RuntimeError("libamdhip64 not found")
+
+
+class _Handle:
+    SIZE = 64  # HIP_IPC_HANDLE_SIZE
+
+
+def _ipc_export(t):
+    """(handle bytes, offset) of a device tensor: the IPC handle names the whole allocation that
+    holds it (torch's caching allocator sub-allocates), the offset locates the tensor in it."""
+    import ctypes
+    hip = _hip()
+    base, size = ctypes.c_void_p(), ctypes.c_size_t()
+    if hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(t.data_ptr())) != 0:
+        raise RuntimeError("hipMemGetAddressRange failed")
+    h = (ctypes.c_char * _Handle.SIZE)()
+    if hip.hipIpcGetMemHandle(ctypes.byref(h), base) != 0:
+        raise RuntimeError("hipIpcGetMemHandle failed (HSA_ENABLE_IPC_MODE_LEGACY=0 is required)")
+    return bytes(h), t.data_ptr() - base.value
+
+
+def _ipc_open(handle, offset):
+    import ctypes
+    hip = _hip()
+    h = (ctypes.c_char * _Handle.SIZE).from_buffer_copy(handle)
+    p = ctypes.c_void_p()
+    if hip.hipIpcOpenMemHandle(ctypes.byref(p), h, ctypes.c_uint(1)) != 0:  # hipIpcMemLazyEnablePeerAccess
+        raise RuntimeError("hipIpcOpenMemHandle failed")
+    return p.value, p.value + offset
+
+
+class PeerGather:
+    """Buffers of the fused peer-store all-gather (include/flexq_hip.h fq_linear_w6ax_gather): two
+    gather buffers fp16 [M_max, N_total] per rank, used alternately, plus the rank's flag words, all
+    IPC-exported and opened by every other rank (xGMI peer mappings on a node; the same device in
+    the one-GPU multi-process tests), and one device fq_gather descriptor per buffer parity.
+
+    `linear(x, image, abits)` runs this rank's column shard of a linear, stores it into every rank's
+    gather buffer, waits until all ranks' shards have arrived and returns the full [M, N_total]
+    output (a view of this rank's gather buffer, valid until the call after next).  Replaces
+    ColumnParallelW6Linear's RCCL all_gather at decode sizes (M <= 32)."""
+
+    def __init__(self, M_max, N_total, group=None, device=None):
+        import ctypes
+        import torch
+        from . import ops  # noqa: F401  (loads the library)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > 8:
+            raise ValueError("at most 8 ranks (FQ_GATHER_MAX_RANKS)")
+        self.M_max, self.N_total, self.group = M_max, N_total, group
+        self.lo, self.hi = shard_range(N_total, self.world, self.rank)
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.dev = dev
+        self.bufs = [torch.zeros((M_max, N_total), dtype=torch.float16, device=dev) for _ in range(2)]
+        self.flags = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.state = torch.zeros(2, dtype=torch.int32, device=dev)  # done, gen
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        mine = [_ipc_export(self.bufs[0]), _ipc_export(self.bufs[1]), _ipc_export(self.flags)]
+        allh = [None] * self.world
+        dist.all_gather_object(allh, mine, group=group)
+        self._opened = []
+        ptrs = []  # per rank q: (buf0, buf1, flags)
+        failure = None
+        try:
+            for q in range(self.world):
+                if q == self.rank:
+                    ptrs.append((self.bufs[0].data_ptr(), self.bufs[1].data_ptr(), self.flags.data_ptr()))
+                    continue
+                row = []
+                for (h, off) in allh[q]:
+                    base, p = _ipc_open(h, off)
+                    self._opened.append(base)
+                    row.append(p)
+                ptrs.append(tuple(row))
+        except Exception as e:  # noqa: BLE001
+            failure = f"rank {self.rank}: {e}"
+        # every rank learns whether every mapping succeeded, so a failure raises on all ranks alike
+        # (no rank may go on to store into, or wait on, a peer that could not map it)
+        fails = [None] * self.world
+        dist.all_gather_object(fails, failure, group=group)
+        if any(fails):
+            self.close()
+            raise RuntimeError("PeerGather: IPC mapping failed: " + "; ".join(f for f in fails if f))
+        # two descriptors (fq_gather, include/flexq_hip.h): buffer parity 0 and 1
+        P8 = ctypes.c_uint64 * 8
+        I4 = ctypes.c_int32 * 4
+
+        class Desc(ctypes.Structure):
+            _fields_ = [("out", P8), ("flags", P8), ("done", ctypes.c_uint64), ("gen", ctypes.c_uint64), ("ints", I4)]
+        self.desc = []
+        for parity in range(2):
+            d = Desc()
+            for q in range(self.world):
+                d.out[q] = ptrs[q][parity]
+                d.flags[q] = ptrs[q][2]
+            d.done = self.state.data_ptr()
+            d.gen = self.state.data_ptr() + 4
+            d.ints = I4(self.world, self.rank, self.lo, N_total)
+            raw = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8)
+            self.desc.append(raw.to(dev))
+        torch.cuda.synchronize(dev)
+        dist.barrier(group=group)  # every rank's buffers are mapped before anyone stores into them
+        self.calls = 0
+
+    def linear(self, x, image, abits=6, parity=None):
+        """x fp16 [M, K] (replicated) -> full output [M, N_total] (this rank's gather buffer).
+        parity: which of the two gather buffers (default: alternate per call); a caller capturing
+        a fixed sequence of calls (a HIP graph) passes it explicitly, alternating per object."""
+        import ctypes
+        import torch
+        from . import _lib, ops
+        M, K = x.shape
+        if M > self.M_max:
+            raise ValueError(f"M={M} > M_max={self.M_max}")
+        n = self.hi - self.lo
+        if parity is None:
+            parity = self.calls & 1
+            self.calls += 1
+        s = ops._stream(x)
+        nb = ops.gemm_workspace_bytes(M, n, K)
+        wbuf = ops.workspace(x.device, nb, s.value)
+        xq = xs = None
+        if ops.act_scratch_bytes(M, n, K):
+            xq = torch.empty((M, K), dtype=torch.int8, device=x.device)
+            xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=x.device)
+        _lib.call("fq_linear_w6ax_gather", ops._ptr(x), M, n, K, abits, ops._ptr(image), ops._ptr(self.desc[parity]),
+                  ops._ptr(xq), ops._ptr(xs), ops._ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+        _lib.call("fq_gather_wait", ops._ptr(self.desc[parity]), ops._ptr(self.err), s)
+        return self.bufs[parity][:M]
+
+    def error(self):
+        """Nonzero when a wait timed out (a rank stopped publishing)."""
+        return int(self.err.item())
+
+    def close(self):
+        hip = _hip()
+        import ctypes
+        for p in self._opened:
+            hip.hipIpcCloseMemHandle(ctypes.c_void_p(p))
+        self._opened = []

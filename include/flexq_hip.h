@@ -149,6 +149,33 @@ fq_status fq_silu_mul_quantize(const uint16_t *gate, const uint16_t *up, int ld,
                                int abits, int8_t *xq, uint16_t *xs, uint16_t *act_out,
                                fq_stream_t stream);
 
+/* ---- column-parallel decode with the all-gather in the GEMM epilogue -------
+ * The north-star N-shard: rank p of P holds columns [col0, col0 + N) of a linear whose full width is
+ * ld.  fq_linear_w6ax_gather computes this rank's columns exactly as fq_linear_w6ax does and stores
+ * them straight into EVERY rank's gather buffer out[q] (fp16 [M][ld], IPC-mapped device pointers:
+ * xGMI peer stores on a node), with system-scope write-through stores; after the launch's last
+ * workgroup has seen every store drained it raises flags[q][rank] = *gen + 1 in every rank.
+ * fq_gather_wait (one small launch) then waits for all P flags of this rank, acquires and advances
+ * *gen: after it, out[rank] holds the whole [M][ld] output.  This replaces the per-linear RCCL
+ * all_gather (nccl_utils.cc:70-82's ftNcclAllGather in the reference) at decode sizes.
+ * Use two gather buffers alternately (linear j writes buffer j % 2): a rank can then run at most
+ * one linear ahead of any other without overwriting an input still being read.  The struct lives
+ * in device memory; done and gen are this rank's own words, zeroed once.  The wait is bounded
+ * (~4 s): on timeout *err is set to 1 and the results are undefined (never a hang).
+ * M <= 32, N % 16 == 0, P <= FQ_GATHER_MAX_RANKS. */
+#define FQ_GATHER_MAX_RANKS 8
+typedef struct fq_gather {
+    uint16_t *out[FQ_GATHER_MAX_RANKS];   /* rank q's gather buffer, fp16 [M][ld] */
+    uint32_t *flags[FQ_GATHER_MAX_RANKS]; /* rank q's flag words, uint32 [P] */
+    uint32_t *done;                       /* this rank's launch ticket */
+    uint32_t *gen;                        /* this rank's generation */
+    int P, rank, col0, ld;
+} fq_gather;
+fq_status fq_linear_w6ax_gather(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
+                                const fq_gather *gather, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
+                                size_t workspace_bytes, fq_stream_t stream);
+fq_status fq_gather_wait(const fq_gather *gather, uint32_t *err, fq_stream_t stream);
+
 /* ---- reference-layout entry points (drop-in for FlexQ's own formats) ------------------------ */
 /* flexq_bit_packing(const int* in, int* out, M, K, BIT, stream) (engine/src/pack/bit_packing.h:34,
  * bit_packing.cu:147-156): raw b-bit patterns [M][K] -> bit planes int32

@@ -58,3 +58,65 @@ def test_column_parallel_linear_multi_process(dev, M, N, K, abits, world):
         assert tuple(res[r].shape) == (M, N)
         assert_gemm_close(res[r].numpy(), ref, mag, f"column-parallel rank {r} of {world}")
         np.testing.assert_array_equal(res[r].numpy().view(np.uint16), res[0].numpy().view(np.uint16))
+
+
+def _peer_worker(rank, world, port, cases, q):
+    import torch.distributed as dist
+    from flexq_amd import dist as fqd
+    from flexq_amd import ops
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        out = {}
+        for (M, N, K, abits, chain) in cases:
+            w = torch.from_numpy(weight_input(N, K, seed=31).astype(np.float16))
+            img, _ = ops.quantize_pack_w6(fqd.shard_weight(w, world, rank).to(dev))
+            ref_lin = fqd.ColumnParallelW6Linear(img, N, K, abits)
+            pg = fqd.PeerGather(M, N, device=dev)
+            x = torch.from_numpy(act_input(M, K, seed=32).astype(np.float16)).to(dev)
+            got, want = [], []
+            for step in range(chain):
+                y = pg.linear(x, img, abits)          # peer-store gather fused into the GEMM epilogue
+                torch.cuda.synchronize()
+                yr = ref_lin(x)                       # the RCCL/gloo all_gather path
+                got.append(y.cpu().numpy().copy())
+                want.append(yr.cpu().numpy())
+                if K == N:
+                    x = y.clone()                     # a dependent chain (next input = this output)
+            out[(M, N, K, abits)] = (got, want, pg.error())
+            pg.close()
+        q.put((rank, out))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_store_gather_matches_all_gather(dev, world):
+    """fq_linear_w6ax_gather + fq_gather_wait (the all-gather fused into the decode GEMM epilogue
+    through IPC-mapped peer buffers) against ColumnParallelW6Linear's all_gather: every rank's full
+    output bit-identical to the collective's, over dependent chains of calls that alternate the two
+    gather buffers, at M = 1 (fused quantizer), M = 4 (split-K shard) and M = 16 (separate quantize)."""
+    import torch.multiprocessing as mp
+    cases = [(1, 2048, 2048, 6, 6), (4, 512, 8192, 8, 3), (16, 4096, 4096, 6, 4)]
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_peer_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p_ in procs:
+        p_.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p_ in procs:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    for (M, N, K, abits, chain) in cases:
+        for r in range(world):
+            got, want, err = res[r][(M, N, K, abits)]
+            assert err == 0, f"rank {r}: a gather wait timed out"
+            assert len(got) == chain
+            for i, (g, w) in enumerate(zip(got, want)):
+                np.testing.assert_array_equal(g.view(np.uint16), w.view(np.uint16), err_msg=f"rank {r} call {i}")
+            np.testing.assert_array_equal(got[-1].view(np.uint16), res[0][(M, N, K, abits)][0][-1].view(np.uint16))
