@@ -63,6 +63,10 @@ _SIGS = {
     "fq_silu_mul_quantize": ([P, P, I, I, I, I, P, P, P, P], I),
     "fq_linear_w6ax_gather": ([P, I, I, I, I, P, P, P, P, P, SZ, P], I),
     "fq_gather_wait": ([P, P, P], I),
+    "fq_rmsnorm_linear_scratch_bytes": ([I, I, I], SZ),
+    "fq_silu_linear_scratch_bytes": ([I, I, I], SZ),
+    "fq_rmsnorm_linear_w6ax": ([P, P, P, P, ctypes.c_float, I, I, I, I, P, P, P, P, P, SZ, P], I),
+    "fq_silu_linear_w6ax": ([P, P, I, I, I, I, I, P, P, P, P, P, SZ, P], I),
 }
 
 

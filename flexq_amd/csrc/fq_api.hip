@@ -7,6 +7,12 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
 fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
                             int abits, uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
                             fq_stream_t stream, const fq_gather *gat);
+fq_status fq_decode_linear_pro(int pro, const uint16_t *xh, const DecodePro &prod, int M, int N, int K, int abits,
+                               const void *w_packed, uint16_t *d, void *workspace, size_t workspace_bytes,
+                               hipStream_t s, bool *launched);
+fq_status fq_rmsnorm_quantize_to(const uint16_t *input, const uint16_t *residual, uint16_t *res_out,
+                                 const uint16_t *gamma, float eps, int M, int K, int abits, int8_t *xq, uint16_t *xs,
+                                 uint16_t *normed_out, fq_stream_t stream);
 
 extern "C" const char *fq_version(void) { return "flexq_amd 0.3.0 (gfx950, int8-MFMA W6Ax)"; }
 extern "C" int fq_abi_version(void) { return FQ_ABI_VERSION; }
@@ -58,6 +64,51 @@ extern "C" fq_status fq_linear_w6ax_gather(const uint16_t *x, int M, int N, int 
     if (st != FQ_OK) return st;
     return fq_gemm_w6ax_impl(xq_buf, xs_buf, w_packed, M, N, K, abits, nullptr, nullptr, workspace,
                              workspace_bytes, stream, gather);
+}
+
+// ---- producers fused into the linear (the caller side of the path) --------
+// One launch at decode sizes (the producer runs in the decode kernel's prologue); otherwise the
+// producer kernel into xq_buf / xs_buf, then the GEMM.  Same bits either way: both run
+// fq_common.h's producer arithmetic and the same quantizer and GEMM plan.
+extern "C" fq_status fq_rmsnorm_linear_w6ax(const uint16_t *input, const uint16_t *residual, uint16_t *residual_out,
+                                            const uint16_t *gamma, float eps, int M, int N, int K, int abits,
+                                            const void *w_packed, uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf,
+                                            void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+    if (!residual || !gamma || !w_packed || !d || (input && !residual_out)) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (input && residual_out == residual) return FQ_ERR_SHAPE;  // other workgroups still read it
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    const uintptr_t al = (uintptr_t)residual | (uintptr_t)gamma | (uintptr_t)input | (uintptr_t)residual_out;
+    if (al & 15) return FQ_ERR_SHAPE;
+    bool launched = false;
+    const DecodePro pro = {input, gamma, residual_out, eps, K};
+    fq_status st = fq_decode_linear_pro(1, residual, pro, M, N, K, abits, w_packed, d, workspace, workspace_bytes,
+                                        (hipStream_t)stream, &launched);
+    if (launched || st != FQ_OK) return st;
+    if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
+    st = fq_rmsnorm_quantize_to(input, residual, input ? residual_out : nullptr, gamma, eps, M, K, abits, xq_buf,
+                                xs_buf, nullptr, stream);
+    if (st != FQ_OK) return st;
+    return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" fq_status fq_silu_linear_w6ax(const uint16_t *gate, const uint16_t *up, int ld, int M, int N, int K,
+                                         int abits, const void *w_packed, uint16_t *d, int8_t *xq_buf,
+                                         uint16_t *xs_buf, void *workspace, size_t workspace_bytes,
+                                         fq_stream_t stream) {
+    if (!gate || !up || !w_packed || !d) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || ld < K || ld % 8 || M > 65535) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    if (((uintptr_t)gate | (uintptr_t)up) & 15) return FQ_ERR_SHAPE;
+    bool launched = false;
+    const DecodePro pro = {up, nullptr, nullptr, 0.0f, ld};
+    fq_status st = fq_decode_linear_pro(2, gate, pro, M, N, K, abits, w_packed, d, workspace, workspace_bytes,
+                                        (hipStream_t)stream, &launched);
+    if (launched || st != FQ_OK) return st;
+    if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
+    st = fq_silu_mul_quantize(gate, up, ld, M, K, abits, xq_buf, xs_buf, nullptr, stream);
+    if (st != FQ_OK) return st;
+    return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace, workspace_bytes, stream);
 }
 
 // ---- FQBMMAOpState-style interface (flexq_bmma_op.h:19-34,163-188) ---------------------------

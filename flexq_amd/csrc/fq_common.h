@@ -154,6 +154,75 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
     return sh;
 }
 
+// ---- producer arithmetic, 8 fp16 values per call: fq_producers.hip's kernels and the decode
+// kernel's fused prologues (fq_gemm.hip, PRO = 1 / 2) share these, so the two give the same bits.
+// half_clamp = clamp_inf_for_half (reduce_kernel_utils.cuh:357-361): clamp to +-(65504 - 1000).
+__device__ __forceinline__ float half_clamp_f(float v) {
+    return v > 0.0f ? fminf(v, 65504.0f - 1000.0f) : fmaxf(v, -65504.0f + 1000.0f);
+}
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+    return (uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16);
+}
+__device__ __forceinline__ float lo_f(uint32_t w) { return h2f((uint16_t)w); }
+__device__ __forceinline__ float hi_f(uint32_t w) { return h2f((uint16_t)(w >> 16)); }
+
+// r = half_clamp(float(in) + float(res))                    (layernorm_kernels.cu:1883)
+__device__ __forceinline__ uint4 add_residual8(uint4 in, uint4 res) {
+    const uint32_t a[4] = {in.x, in.y, in.z, in.w}, b[4] = {res.x, res.y, res.z, res.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        o[i] = pack_h2(half_clamp_f(lo_f(a[i]) + lo_f(b[i])), half_clamp_f(hi_f(a[i]) + hi_f(b[i])));
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+// acc += float(r)^2 over the 8 values in order (fmaf)
+__device__ __forceinline__ float sumsq8(uint4 r, float acc) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float v0 = lo_f(w[i]), v1 = hi_f(w[i]);
+        acc = fmaf(v0, v0, acc);
+        acc = fmaf(v1, v1, acc);
+    }
+    return acc;
+}
+// 1 / sqrt(ss / K + eps), IEEE (the reference uses rsqrtf, layernorm_kernels.cu:1890)
+__device__ __forceinline__ float rms_scale(float ss, int K, float eps) {
+    return 1.0f / __builtin_sqrtf(ss / (float)K + eps);
+}
+// normed = half_clamp((float(r) * rs) * float(gamma)), two roundings     (:1898)
+__device__ __forceinline__ uint4 rms_apply8(uint4 r, uint4 g, float rs) {
+    const uint32_t a[4] = {r.x, r.y, r.z, r.w}, gm[4] = {g.x, g.y, g.z, g.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        o[i] = pack_h2(half_clamp_f(__fmul_rn(__fmul_rn(lo_f(a[i]), rs), lo_f(gm[i]))),
+                       half_clamp_f(__fmul_rn(__fmul_rn(hi_f(a[i]), rs), hi_f(gm[i]))));
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+// act = half(silu(float(gate)) * float(up)), silu(v) = v / (1 + exp(-v)) with the hardware's fast
+// exp, as the reference's __expf                   (activation_kernels.cu:133, 300)
+__device__ __forceinline__ uint4 silu_mul8(uint4 g4, uint4 u4) {
+    const uint32_t g[4] = {g4.x, g4.y, g4.z, g4.w}, u[4] = {u4.x, u4.y, u4.z, u4.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float g0 = lo_f(g[i]), g1 = hi_f(g[i]);
+        const float s0 = g0 / (1.0f + __expf(-g0)), s1 = g1 / (1.0f + __expf(-g1));
+        o[i] = pack_h2(__fmul_rn(s0, lo_f(u[i])), __fmul_rn(s1, hi_f(u[i])));
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// arguments of a producer fused into the decode linear's prologue (fq_gemm.hip, PRO = 1 / 2)
+struct DecodePro {
+    const uint16_t *in;     // PRO 1: added to the residual (or null); PRO 2: up
+    const uint16_t *gamma;  // PRO 1
+    uint16_t *res_out;      // PRO 1 with `in`: residual + in (never the residual itself)
+    float eps;              // PRO 1
+    int ldh;                // row stride (elements) of xh and `in` (PRO 2; K otherwise)
+};
+
 // ---- fq6 weight unpack ----------------------------------------------------------------------
 // Three packed dwords -> the 16-byte MFMA B operand, every byte = 4*w (w in the top 6 bits).
 // Layout contract: oracle/fq_oracle.c fqo_pack_fq6 and DESIGN.md §3.

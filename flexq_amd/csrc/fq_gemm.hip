@@ -92,12 +92,13 @@ __host__ __device__ inline int decode_slot(int MT, int XS, int SS) {
 __host__ __device__ inline int decode_xwin_bytes(int ng, int M, int xwin) { return (ng * M < xwin ? (ng * M + 3) / 4 * 4 : xwin) * 256; }
 // per-wave LDS: [ring D x SLOT][ws: nb x 8 dwords][xs: ng x XSR dwords][x: ng x M x 128 B]
 //               [FUSE: fp16 window]
-__host__ __device__ inline int decode_wave_lds(int MT, int XS, int SS, int ng, int nb, int M, int xwin) {
+// (wm windows side by side: 3 for the RMSNorm prologue -- residual, input, gamma --, 2 for SiLU * up)
+__host__ __device__ inline int decode_wave_lds(int MT, int XS, int SS, int ng, int nb, int M, int xwin, int wm = 1) {
     const int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;
     int b = decode_depth_for(MT, XS, decode_slot(MT, XS, SS), 2 + XP + (SS ? 2 : 0)) * decode_slot(MT, XS, SS);
     if (!SS) b += decode_wsst_bytes(nb) + decode_xsst_bytes(ng, MT);
     if (!XS) b += decode_xst_bytes(ng, M);
-    if (xwin) b += decode_xwin_bytes(ng, M, xwin);
+    if (xwin) b += wm * decode_xwin_bytes(ng, M, xwin);
     return b;
 }
 
@@ -210,15 +211,25 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
     }
 }
 
+// Producer fused into the FUSE prologue (fq_rmsnorm_linear_w6ax / fq_silu_linear_w6ax):
+//   PRO = 1: xh is the residual; r = half_clamp(in + residual) when `in`, RMSNorm with gamma, then
+//            the quantizer (M = 1, K = 4 * 128 * NW, S = 1: wave w's four groups are exactly the
+//            512-thread producer's chunks 64w .. 64w + 63, so the sum of squares is formed in the
+//            same order -- per lane, the 64-lane butterfly, the waves in order -- and the codes are
+//            fq_rmsnorm_quantize's bits).  Workgroup 0 writes r to res_out.
+//   PRO = 2: xh is the gate, `in` the up projection (row stride ldh): act = half(silu(gate) * up).
+// The arithmetic is fq_common.h's, shared with fq_producers.hip.
+// (DecodePro: fq_common.h)
+
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
-template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false>
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0>
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
     float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir,
-    int NCH, const fq_gather *__restrict__ gat) {
+    int NCH, const fq_gather *__restrict__ gat, const DecodePro pro) {
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
     // second serial round trip before the first DMA; tools/stamps.py).
@@ -228,6 +239,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     using C = DecodeCfg<MT, XS, SS>;
     constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
     static_assert(!FUSE || (XS == 0 && SS == 0), "fused quantization stages into LDS");
+    static_assert(PRO == 0 || (FUSE && !CH), "fused producers run in the fused quantizer's prologue");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FQ_STAMP(0);
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
@@ -263,7 +275,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     // blocked w-scales of the image: fp16 [NT][G][16] after the weight blocks (fq_quant.hip)
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
 
-    const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, FUSE ? xwin : 0);
+    const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, FUSE ? xwin : 0, PRO == 1 ? 3 : PRO == 2 ? 2 : 1);
     char *ring = smem + wid * wl;
     char *ws_st = ring + D * C::SLOT;                                 // staged w-scales
     char *xs_st = ws_st + (SS ? 0 : decode_wsst_bytes(ngmax * IPW));  // staged x-scales
@@ -271,6 +283,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int EM = M * 16;                                            // live elements of a tile
     float *red = reinterpret_cast<float *>(smem + NW * wl);           // [RC][NW][M*16]
     int *flag = reinterpret_cast<int *>(red + RC * NW * EM);          // [IPW]
+    char *wsum = reinterpret_cast<char *>(flag) + ((4 * IPW + 15) & ~15);  // PRO 1: [NW] floats
 
     auto item_tile = [&](int it) { return t0 + it * tstep; };
 
@@ -280,13 +293,21 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     const int qsub = lane & 15;
     const int R = ng * M;  // (group, row) pairs this wave quantizes
     char *xh_st = x_st + (XS ? 0 : decode_xst_bytes(ngmax, M));  // fp16 window (FUSE)
+    const int xwb = FUSE ? decode_xwin_bytes(ngmax, M, xwin) : 0;   // (PRO: the next windows)
+    const long ldh = PRO ? (long)pro.ldh : (long)K;
     auto x_fetch = [&](int r0) {  // pairs [r0, r0 + xwin) -> xh_st
         for (int c = 0; c < xwin && r0 + c < R; c += 4) {
             int rg = r0 + c + (lane >> 4);
             rg = rg < R ? rg : R - 1;
             const int j = M == 1 ? rg : rg / M, row = rg - j * M;
-            __builtin_amdgcn_global_load_lds(xh + (long)row * K + (long)(ga + j) * FQ_GROUP + qsub * 8,
-                                             LDS_PTR(xh_st + c * 256), 16, 0, 0);
+            const long off = (long)(ga + j) * FQ_GROUP + qsub * 8;
+            __builtin_amdgcn_global_load_lds(xh + row * ldh + off, LDS_PTR(xh_st + c * 256), 16, 0, 0);
+            if (PRO == 1 && pro.in)
+                __builtin_amdgcn_global_load_lds(pro.in + off, LDS_PTR(xh_st + xwb + c * 256), 16, 0, 0);
+            if (PRO == 1)
+                __builtin_amdgcn_global_load_lds(pro.gamma + off, LDS_PTR(xh_st + 2 * xwb + c * 256), 16, 0, 0);
+            if (PRO == 2)
+                __builtin_amdgcn_global_load_lds(pro.in + row * ldh + off, LDS_PTR(xh_st + xwb + c * 256), 16, 0, 0);
         }
     };
     auto x_store = [&](int rg, uint2 codes, uint16_t sh) {
@@ -302,14 +323,25 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             const bool two = c + 4 < xwin && r0 + c + 4 < R;
             v4i raw0 = ds_read_b128(lds_addr(xh_st + c * 256 + lane * 16));
             v4i raw1 = ds_read_b128(lds_addr(xh_st + (two ? c + 4 : c) * 256 + lane * 16));
-            // the wait redefines raw0/raw1, so no use of them can be placed above it
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(raw0), "+v"(raw1)::"memory");
+            v4i up0, up1;  // PRO 2: the up window
+            if (PRO == 2) {
+                up0 = ds_read_b128(lds_addr(xh_st + xwb + c * 256 + lane * 16));
+                up1 = ds_read_b128(lds_addr(xh_st + xwb + (two ? c + 4 : c) * 256 + lane * 16));
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(raw0), "+v"(raw1), "+v"(up0), "+v"(up1)::"memory");
+            } else {
+                // the wait redefines raw0/raw1, so no use of them can be placed above it
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(raw0), "+v"(raw1)::"memory");
+            }
+            uint4 v0 = make_uint4(raw0[0], raw0[1], raw0[2], raw0[3]);
+            if (PRO == 2) v0 = silu_mul8(v0, make_uint4(up0[0], up0[1], up0[2], up0[3]));
             uint2 codes0;
-            const uint16_t sh0 = quant_group16(make_uint4(raw0[0], raw0[1], raw0[2], raw0[3]), abits, codes0);
+            const uint16_t sh0 = quant_group16(v0, abits, codes0);
             x_store(rg, codes0, sh0);
             if (two) {
+                uint4 v1 = make_uint4(raw1[0], raw1[1], raw1[2], raw1[3]);
+                if (PRO == 2) v1 = silu_mul8(v1, make_uint4(up1[0], up1[1], up1[2], up1[3]));
                 uint2 codes1;
-                const uint16_t sh1 = quant_group16(make_uint4(raw1[0], raw1[1], raw1[2], raw1[3]), abits, codes1);
+                const uint16_t sh1 = quant_group16(v1, abits, codes1);
                 x_store(rg + 4, codes1, sh1);
             }
         }
@@ -391,7 +423,33 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
     if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
         wait_vm_plus<D * C::U>(nws);
         FQ_STAMP(5);
-        x_quant(0);
+        if (PRO == 1) {  // residual add + RMSNorm over the row (R = 4 pairs: lane = chunk 64 wid + lane)
+            const uint32_t xb = lds_addr(xh_st) + lane * 16;
+            v4i rr = ds_read_b128(xb), ii = ds_read_b128(xb + xwb), gg = ds_read_b128(xb + 2 * xwb);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rr), "+v"(ii), "+v"(gg)::"memory");
+            uint4 r = make_uint4(rr[0], rr[1], rr[2], rr[3]);
+            if (pro.in) {
+                r = add_residual8(make_uint4(ii[0], ii[1], ii[2], ii[3]), r);
+                if (blockIdx.x == 0) *reinterpret_cast<uint4 *>(pro.res_out + 8 * (64 * wid + lane)) = r;
+            }
+            float acc = sumsq8(r, 0.0f);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+            if (lane == 0) ds_write_b32(lds_addr(wsum) + 4 * wid, __float_as_uint(acc));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            v4i s0 = ds_read_b128(lds_addr(wsum)), s1 = ds_read_b128(lds_addr(wsum) + 16);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s0), "+v"(s1)::"memory");
+            float ss = __int_as_float(s0[0]);
+#pragma unroll
+            for (int w = 1; w < NW; w++) ss = ss + __int_as_float(w < 4 ? s0[w] : s1[w - 4]);
+            uint2 codes;
+            const uint16_t sh = quant_group16(rms_apply8(r, make_uint4(gg[0], gg[1], gg[2], gg[3]), rms_scale(ss, K, pro.eps)),
+                                              abits, codes);
+            x_store(lane >> 4, codes, sh);
+        } else {
+            x_quant(0);
+        }
         FQ_STAMP(6);
         if (ABL & 32) {  // development: the same code once more (instruction cache now warm);
             if (!(ABL & 64)) x_quant(0);  // with 64: nothing, i.e. the cost of a stamp itself
@@ -1209,6 +1267,7 @@ struct DecodePlan {
     int NCH;                                 // row chunks of MT rows (M > 32), else 1
     int NT;                                  // 16-column tiles
     int cost4;                               // modelled time, quarter-blocks per wave (see decode_plan)
+    int pro;                                 // fused producer (DecodePro): 0, 1 (RMSNorm) or 2 (SiLU)
     bool fits;
 };
 static const size_t kLdsMax = 160 * 1024;
@@ -1229,8 +1288,9 @@ static size_t decode_lds_bytes(const DecodePlan &p, int M, int N, int K) {
     const int NW = decode_waves(p.MT);
     const int Gz = (K / FQ_GROUP + p.S - 1) / p.S;
     const int ngmax = (Gz + NW - 1) / NW;
-    return (size_t)NW * decode_wave_lds(p.MT, p.XS, p.SS, ngmax, ngmax * p.IPW, M, p.xwin) +
-           (size_t)p.RC * NW * M * 16 * 4 + 4 * (size_t)p.IPW + 16;
+    const int wm = p.pro == 1 ? 3 : p.pro == 2 ? 2 : 1;
+    return (size_t)NW * decode_wave_lds(p.MT, p.XS, p.SS, ngmax, ngmax * p.IPW, M, p.xwin, wm) +
+           (size_t)p.RC * NW * M * 16 * 4 + ((4 * (size_t)p.IPW + 15) & ~(size_t)15) + 4 * NW + 16;
 }
 
 // Cost model, in quarter-blocks of one wave's stream (one 1.5 KiB block per wave at the
@@ -1244,8 +1304,9 @@ static const int kSplitQuantCost4 = 12;
 
 // fused: only the fully staged variant (the quantizer writes straight into the staged regions);
 // `fits` is false when that does not fit LDS and the caller must quantize separately.
-static DecodePlan decode_plan(int M, int N, int K, bool fused) {
+static DecodePlan decode_plan(int M, int N, int K, bool fused, int pro = 0) {
     DecodePlan p;
+    p.pro = fused ? pro : 0;
     p.MT = M <= 4 ? 4 : (M <= 8 ? 8 : (M <= 16 ? 16 : 32));
     const int NT = (N + 15) / 16, G = K / FQ_GROUP;
     p.NT = NT;
@@ -1435,9 +1496,10 @@ struct DecodeArgs {
     int32_t *acc_dbg;
     void *workspace;
     const fq_gather *gat;  // peer-store gather (device memory), or nullptr
+    DecodePro pro;         // fused producer arguments (PRO > 0)
 };
 
-template <int MT, int XS, int SS, bool FUSE, bool DBG, bool CH = false>
+template <int MT, int XS, int SS, bool FUSE, bool DBG, bool CH = false, int PRO = 0>
 static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
     uint32_t *tickets = p.S > 1 ? (uint32_t *)a.workspace : nullptr;
     float *slabs = p.S > 1 ? (float *)((char *)a.workspace + kTicketBytes) : nullptr;
@@ -1451,7 +1513,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
                            a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
                            slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),              \
-                           p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat);                                        \
+                           p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat, a.pro);                                 \
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
@@ -1459,9 +1521,10 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 #undef FQ_ABL
     }
 #endif
-    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH>), grid, block, lds, stream, a.xq, a.xs, a.xh,
-                       a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S, p.IPW,
-                       p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat);
+    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH, PRO>), grid, block, lds, stream, a.xq, a.xs,
+                       a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S,
+                       p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH,
+                       a.gat, a.pro);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
@@ -1492,9 +1555,9 @@ static fq_status dispatch_decode(const DecodePlan &p, const DecodeArgs &a, hipSt
 
 // The fused one-launch linear is taken when it fits and its modelled cost (in-kernel quantizer
 // redundant across WGs) does not exceed the split plan's (quantize launch + GEMM).
-static bool decode_fuse(int M, int N, int K, DecodePlan *out) {
+static bool decode_fuse(int M, int N, int K, DecodePlan *out, int pro = 0) {
     if (M > 32) return false;
-    const DecodePlan f = decode_plan(M, N, K, true);
+    const DecodePlan f = decode_plan(M, N, K, true, pro);
     if (!f.fits || f.cost4 > decode_plan(M, N, K, false).cost4) return false;
     if (out) *out = f;
     return true;
@@ -1515,9 +1578,48 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
     if (!decode_fuse(M, N, K, &p)) return FQ_OK;
     const size_t need = fq_gemm_workspace_bytes(M, N, K);
     if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
-    DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace, gat};
+    DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace, gat, DecodePro{}};
     *launched = true;
     return acc_dbg ? dispatch_decode<true, true>(p, a, s) : dispatch_decode<true, false>(p, a, s);
+}
+
+// A producer fused into the one-launch decode linear (DecodePro): pro = 1, residual add + RMSNorm
+// (xh = the residual; M = 1, K = 4 * 128 * waves, no k-split), pro = 2, SiLU(xh) * in (M <= 32).
+// Launches only when the fused plan is taken; *launched tells the caller to run the producer
+// kernel and the GEMM instead.
+static bool pro_fuse(int pro, int M, int N, int K, DecodePlan *p) {
+    if (!decode_fuse(M, N, K, p, pro)) return false;
+    return pro != 1 || (M == 1 && p->MT == 4 && p->S == 1 && K == 4 * FQ_GROUP * decode_waves(4));
+}
+extern "C" size_t fq_rmsnorm_linear_scratch_bytes(int M, int N, int K) {
+    DecodePlan p;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || pro_fuse(1, M, N, K, &p)) return 0;
+    return (size_t)M * K + (size_t)M * (K / FQ_GROUP) * 2;
+}
+extern "C" size_t fq_silu_linear_scratch_bytes(int M, int N, int K) {
+    DecodePlan p;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || pro_fuse(2, M, N, K, &p)) return 0;
+    return (size_t)M * K + (size_t)M * (K / FQ_GROUP) * 2;
+}
+
+fq_status fq_decode_linear_pro(int pro, const uint16_t *xh, const DecodePro &prod, int M, int N, int K, int abits,
+                               const void *w_packed, uint16_t *d, void *workspace, size_t workspace_bytes,
+                               hipStream_t s, bool *launched) {
+    *launched = false;
+    if (pro != 1 && pro != 2) return FQ_ERR_SHAPE;
+    DecodePlan p;
+    if (!pro_fuse(pro, M, N, K, &p)) return FQ_OK;
+    const size_t need = fq_gemm_workspace_bytes(M, N, K);
+    if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
+    DecodeArgs a = {nullptr, nullptr, xh, abits, w_packed, M, N, K, d, nullptr, workspace, nullptr, prod};
+    *launched = true;
+    if (pro == 1) return launch_decode<4, 0, 0, true, false, false, 1>(p, a, s);
+    switch (p.MT) {
+        case 4: return launch_decode<4, 0, 0, true, false, false, 2>(p, a, s);
+        case 8: return launch_decode<8, 0, 0, true, false, false, 2>(p, a, s);
+        case 16: return launch_decode<16, 0, 0, true, false, false, 2>(p, a, s);
+        default: return launch_decode<32, 0, 0, true, false, false, 2>(p, a, s);
+    }
 }
 
 fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,

@@ -38,15 +38,6 @@
 constexpr int PR_THREADS = 256;  // SiLU kernel
 constexpr int PR_KMAX = 32768;   // RMSNorm rows: T * 8 * MAXCH = 32768 for every T
 
-__device__ __forceinline__ float half_clamp_f(float v) {
-    return v > 0.0f ? fminf(v, 65504.0f - 1000.0f) : fmaxf(v, -65504.0f + 1000.0f);
-}
-__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
-    return (uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16);
-}
-__device__ __forceinline__ float lo_f(uint32_t w) { return h2f((uint16_t)w); }
-__device__ __forceinline__ float hi_f(uint32_t w) { return h2f((uint16_t)(w >> 16)); }
-
 // the 16 lanes of a group quantize and store their codes and the group's scale
 __device__ __forceinline__ void quant_store(uint4 vals, int abits, bool valid, int8_t *xq_row_chunk,
                                             uint16_t *xs_slot, bool first_lane) {
@@ -60,11 +51,11 @@ __device__ __forceinline__ void quant_store(uint4 vals, int abits, bool valid, i
 
 template <int T>
 __global__ __launch_bounds__(T) void fq_rmsnorm_quant_kernel(const uint16_t *__restrict__ input,
-                                                                      uint16_t *__restrict__ residual,
-                                                                      const uint16_t *__restrict__ gamma, float eps,
-                                                                      int M, int K, int abits, int8_t *__restrict__ xq,
-                                                                      uint16_t *__restrict__ xs,
-                                                                      uint16_t *__restrict__ normed) {
+                                                             const uint16_t *residual, uint16_t *res_out,
+                                                             const uint16_t *__restrict__ gamma, float eps,
+                                                             int M, int K, int abits, int8_t *__restrict__ xq,
+                                                             uint16_t *__restrict__ xs,
+                                                             uint16_t *__restrict__ normed) {
     constexpr int MAXCH = PR_KMAX / 8 / T;
     __shared__ float wsum[T / 64];
     const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -79,24 +70,12 @@ __global__ __launch_bounds__(T) void fq_rmsnorm_quant_kernel(const uint16_t *__r
         if (c * T < nq && q < nq) {
             gm[c] = *reinterpret_cast<const uint4 *>(gamma + 8 * (size_t)q);  // in flight with the row
             uint4 res = *reinterpret_cast<const uint4 *>(residual + row + 8 * (size_t)q);
-            if (input) {
-                const uint4 in = *reinterpret_cast<const uint4 *>(input + row + 8 * (size_t)q);
-                const uint32_t a[4] = {in.x, in.y, in.z, in.w}, b[4] = {res.x, res.y, res.z, res.w};
-                uint32_t o[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    o[i] = pack_h2(half_clamp_f(lo_f(a[i]) + lo_f(b[i])), half_clamp_f(hi_f(a[i]) + hi_f(b[i])));
-                res = make_uint4(o[0], o[1], o[2], o[3]);
-                *reinterpret_cast<uint4 *>(residual + row + 8 * (size_t)q) = res;
+            if (input) {  // (res_out may be the residual itself: each thread owns its chunks)
+                res = add_residual8(*reinterpret_cast<const uint4 *>(input + row + 8 * (size_t)q), res);
+                *reinterpret_cast<uint4 *>(res_out + row + 8 * (size_t)q) = res;
             }
             r[c] = res;
-            const uint32_t w[4] = {res.x, res.y, res.z, res.w};
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const float v0 = lo_f(w[i]), v1 = hi_f(w[i]);
-                acc = fmaf(v0, v0, acc);
-                acc = fmaf(v1, v1, acc);
-            }
+            acc = sumsq8(res, acc);
         }
     }
 #pragma unroll
@@ -106,7 +85,7 @@ __global__ __launch_bounds__(T) void fq_rmsnorm_quant_kernel(const uint16_t *__r
     float ss = wsum[0];
 #pragma unroll
     for (int w = 1; w < T / 64; w++) ss = ss + wsum[w];
-    const float rs = 1.0f / __builtin_sqrtf(ss / (float)K + eps);
+    const float rs = rms_scale(ss, K, eps);
 #pragma unroll
     for (int c = 0; c < MAXCH; c++) {
         if (c * T >= nq) break;  // block-uniform
@@ -114,13 +93,7 @@ __global__ __launch_bounds__(T) void fq_rmsnorm_quant_kernel(const uint16_t *__r
         const bool valid = q < nq;  // whole 16-lane groups (nq % 16 == 0)
         uint4 nv = make_uint4(0, 0, 0, 0);
         if (valid) {
-            const uint32_t a[4] = {r[c].x, r[c].y, r[c].z, r[c].w}, g[4] = {gm[c].x, gm[c].y, gm[c].z, gm[c].w};
-            uint32_t o[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                o[i] = pack_h2(half_clamp_f(__fmul_rn(__fmul_rn(lo_f(a[i]), rs), lo_f(g[i]))),
-                               half_clamp_f(__fmul_rn(__fmul_rn(hi_f(a[i]), rs), hi_f(g[i]))));
-            nv = make_uint4(o[0], o[1], o[2], o[3]);
+            nv = rms_apply8(r[c], gm[c], rs);
             if (normed) *reinterpret_cast<uint4 *>(normed + row + 8 * (size_t)q) = nv;
         }
         const int gidx = q >> 4;  // 128-group of this chunk
@@ -139,17 +112,8 @@ __global__ __launch_bounds__(PR_THREADS) void fq_silu_mul_quant_kernel(const uin
     const bool valid = q < nq;  // whole 16-lane groups (nq % 16 == 0)
     uint4 av = make_uint4(0, 0, 0, 0);
     if (valid) {
-        const uint4 g4 = *reinterpret_cast<const uint4 *>(gate + (size_t)m * ld + 8 * (size_t)q);
-        const uint4 u4 = *reinterpret_cast<const uint4 *>(up + (size_t)m * ld + 8 * (size_t)q);
-        const uint32_t g[4] = {g4.x, g4.y, g4.z, g4.w}, u[4] = {u4.x, u4.y, u4.z, u4.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const float g0 = lo_f(g[i]), g1 = hi_f(g[i]);
-            const float s0 = g0 / (1.0f + __expf(-g0)), s1 = g1 / (1.0f + __expf(-g1));
-            o[i] = pack_h2(__fmul_rn(s0, lo_f(u[i])), __fmul_rn(s1, hi_f(u[i])));
-        }
-        av = make_uint4(o[0], o[1], o[2], o[3]);
+        av = silu_mul8(*reinterpret_cast<const uint4 *>(gate + (size_t)m * ld + 8 * (size_t)q),
+                       *reinterpret_cast<const uint4 *>(up + (size_t)m * ld + 8 * (size_t)q));
         if (act) *reinterpret_cast<uint4 *>(act + (size_t)m * N + 8 * (size_t)q) = av;
     }
     quant_store(av, abits, valid, xq + (size_t)m * N + 8 * (size_t)q, xs + (size_t)(q >> 4) * M + m,
@@ -158,19 +122,21 @@ __global__ __launch_bounds__(PR_THREADS) void fq_silu_mul_quant_kernel(const uin
 
 static bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
-extern "C" fq_status fq_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const uint16_t *gamma, float eps,
-                                         int M, int K, int abits, int8_t *xq, uint16_t *xs, uint16_t *normed_out,
-                                         fq_stream_t stream) {
-    if (!residual || !gamma || !xq || !xs) return FQ_ERR_NULL;
+// residual + input -> res_out (which may be the residual itself: fq_rmsnorm_quantize's in-place
+// form); fq_rmsnorm_linear_w6ax's unfused path writes a separate buffer.
+fq_status fq_rmsnorm_quantize_to(const uint16_t *input, const uint16_t *residual, uint16_t *res_out,
+                                 const uint16_t *gamma, float eps, int M, int K, int abits, int8_t *xq, uint16_t *xs,
+                                 uint16_t *normed_out, fq_stream_t stream) {
+    if (!residual || !gamma || !xq || !xs || (input && !res_out)) return FQ_ERR_NULL;
     if (M <= 0 || K <= 0 || K % FQ_GROUP || K > PR_KMAX) return FQ_ERR_SHAPE;
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     if (!aligned16(residual) || !aligned16(gamma) || !aligned16(xq) || (input && !aligned16(input)) ||
-        (normed_out && !aligned16(normed_out)))
+        (input && !aligned16(res_out)) || (normed_out && !aligned16(normed_out)))
         return FQ_ERR_SHAPE;
     const int nq = K / 8;  // the oracle (fqo_rmsnorm_quantize) sizes T the same way
 #define FQ_RMS_LAUNCH(T)                                                                                         \
-    hipLaunchKernelGGL(fq_rmsnorm_quant_kernel<T>, dim3(M), dim3(T), 0, (hipStream_t)stream, input, residual, gamma, \
-                       eps, M, K, abits, xq, xs, normed_out)
+    hipLaunchKernelGGL(fq_rmsnorm_quant_kernel<T>, dim3(M), dim3(T), 0, (hipStream_t)stream, input, residual, \
+                       res_out, gamma, eps, M, K, abits, xq, xs, normed_out)
     if (nq <= 256)
         FQ_RMS_LAUNCH(256);
     else if (nq <= 512)
@@ -180,6 +146,12 @@ extern "C" fq_status fq_rmsnorm_quantize(const uint16_t *input, uint16_t *residu
 #undef FQ_RMS_LAUNCH
     FQ_LAUNCH_CHECK();
     return FQ_OK;
+}
+
+extern "C" fq_status fq_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const uint16_t *gamma, float eps,
+                                         int M, int K, int abits, int8_t *xq, uint16_t *xs, uint16_t *normed_out,
+                                         fq_stream_t stream) {
+    return fq_rmsnorm_quantize_to(input, residual, residual, gamma, eps, M, K, abits, xq, xs, normed_out, stream);
 }
 
 extern "C" fq_status fq_silu_mul_quantize(const uint16_t *gate, const uint16_t *up, int ld, int M, int N, int abits,

@@ -98,6 +98,17 @@ class FlexQFfn:
             return y, dict(xq=xq, xs=xs, gate_up=gu, aq=aq, as_=as_)
         return y
 
+    def fused(self, residual, attn_out, residual_out, reduce=True):
+        """run_layers' form of __call__, the same bits: residual + attn_out goes to residual_out
+        (not in place), the norm runs inside gate_up's GEMM and SiLU * up inside down_proj's (one
+        launch each at decode sizes; ops.rmsnorm_linear_w6ax / silu_linear_w6ax).  Returns (y, the
+        updated residual)."""
+        gu, h = ops.rmsnorm_linear_w6ax(residual, self.gamma, self.gate_up.image, self.gate_up.N,
+                                        self.gate_up.abits, eps=self.eps, input=attn_out,
+                                        residual_out=residual_out if attn_out is not None else None)
+        y = ops.silu_linear_w6ax(gu[:, :self.F], gu[:, self.F:], self.down.image, self.down.N, self.down.abits)
+        return self.down._finish(y, reduce), h
+
 
 def _layer_files(out_dir, layer, rank):
     m = json.load(open(os.path.join(out_dir, "manifest.json")))
@@ -139,6 +150,21 @@ class FlexQDecoderLayer:
         ctx = self.attn_fn(self.qkv.from_codes(xq, xs))
         return self.o(ctx.contiguous(), reduce=reduce)
 
+    def step(self, h, pending, spare, reduce=True):
+        """run_layers' form of one layer (defer=True, the same bits): the two fused residual adds
+        write the other of two residual buffers (h, spare) instead of updating h in place -- a
+        decode GEMM's other workgroups are still reading h -- and both norms and SiLU * up run
+        inside their GEMMs (layer = qkv, o_proj, gate_up, down_proj: four launches at M = 1 plus
+        the attention core).  Returns (y to pass as the next `pending`, the residual, the free
+        buffer)."""
+        qkv, h1 = ops.rmsnorm_linear_w6ax(h, self.gamma_attn, self.qkv.image, self.qkv.N, self.qkv.abits,
+                                         eps=self.eps, input=pending,
+                                         residual_out=spare if pending is not None else None)
+        free = h if pending is not None else spare
+        a = self.o(self.attn_fn(qkv).contiguous(), reduce=reduce)
+        y, h2 = self.ffn.fused(h1, a, free, reduce=reduce)
+        return y, h2, h1
+
     def __call__(self, h, pending=None, defer=False, reduce=True):
         """h fp16 [M, H], updated in place to the layer output and returned.  With defer=True the
         final residual add is left to the caller: the FFN output y is returned instead (h holds
@@ -154,16 +180,17 @@ class FlexQDecoderLayer:
 
 def run_layers(layers, h, reduce=True):
     """Run decoder layers in order on h (in place), each layer's final residual add fused into the
-    next layer's pre-attention norm; returns h.  reduce=False (no all-reduces) is a single-rank /
+    next layer's pre-attention norm, the norms and SiLU * up fused into their GEMMs
+    (FlexQDecoderLayer.step; the residual alternates between h and one scratch buffer); returns h.  reduce=False (no all-reduces) is a single-rank /
     timing mode: with more than one rank the unreduced partial sums would feed the next layer's
     norm, so it is rejected there."""
     if not reduce and dist.is_initialized() and any(
             L.o.row_parallel and dist.get_world_size(L.o.group) > 1 for L in layers):
         raise ValueError("run_layers(reduce=False) is single-rank only: with more than one rank every "
                          "layer's input must be the all-reduced sum")
-    pending = None
+    pending, cur, spare = None, h, torch.empty_like(h)
     for L in layers:
-        pending = L(h, pending=pending, defer=True, reduce=reduce)
+        pending, cur, spare = L.step(cur, pending, spare, reduce=reduce)
     if pending is not None:
-        h += pending
+        torch.add(cur, pending, out=h)  # (cur may be h itself: an elementwise in-place add)
     return h

@@ -261,6 +261,82 @@ def silu_mul_quantize(gate, up, abits, return_act=False):
     return (xq, xs, act) if return_act else (xq, xs)
 
 
+def _act_scratch(fn, M, N, K, dev):
+    if not int(getattr(_lib.load(), fn)(M, N, K)):
+        return None, None  # the producer runs inside the decode GEMM: no activation scratch
+    return (torch.empty((M, K), dtype=torch.int8, device=dev),
+            torch.empty((K // GROUP, M), dtype=torch.float16, device=dev))
+
+
+def _out_ok(out, M, N, dev):
+    if out is None:
+        return torch.empty((M, N), dtype=torch.float16, device=dev)
+    _dev(out, torch.float16, "out", 2)
+    _need(tuple(out.shape) == (M, N) and out.device == dev, f"out must be [M, N] = {(M, N)} on {dev}")
+    return out
+
+
+def rmsnorm_linear_w6ax(residual, gamma, wpk, N, abits=6, eps=1e-6, input=None, residual_out=None, out=None):
+    """Residual add + RMSNorm + quantize + W6Ax GEMM (fq_rmsnorm_linear_w6ax): one launch at
+    decode sizes (M = 1, K = 4096), else fq_rmsnorm_quantize + GEMM -- the same bits either way.
+    With input, residual + input is written to residual_out (allocated when None; never the
+    residual itself).  Returns (d fp16 [M, N], the updated residual: residual_out, or residual
+    when input is None)."""
+    _dev(residual, torch.float16, "residual", 2)
+    M, K = residual.shape
+    _k_ok(K)
+    dev = residual.device
+    _dev(gamma, torch.float16, "gamma", 1)
+    _need(gamma.numel() == K and gamma.device == dev, "gamma must be [K] on the residual's device")
+    _img_ok(wpk, N, K)
+    _need(wpk.device == dev, "the weight image must be on the residual's device")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    if input is not None:
+        _dev(input, torch.float16, "input", 2)
+        _need(tuple(input.shape) == (M, K) and input.device == dev, "input must match residual")
+        if residual_out is None:
+            residual_out = torch.empty_like(residual)
+        _dev(residual_out, torch.float16, "residual_out", 2)
+        _need(tuple(residual_out.shape) == (M, K) and residual_out.device == dev, "residual_out must match residual")
+        _need(residual_out.data_ptr() != residual.data_ptr(), "residual_out must not be the residual")
+    else:
+        residual_out = None
+    out = _out_ok(out, M, N, dev)
+    xq, xs = _act_scratch("fq_rmsnorm_linear_scratch_bytes", M, N, K, dev)
+    s = _stream(residual)
+    wbuf = workspace(dev, gemm_workspace_bytes(M, N, K), s.value)
+    _lib.call("fq_rmsnorm_linear_w6ax", _ptr(input), _ptr(residual), _ptr(residual_out), _ptr(gamma),
+              ctypes.c_float(eps), M, N, K, abits, _ptr(wpk), _ptr(out), _ptr(xq), _ptr(xs), _ptr(wbuf),
+              ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return out, (residual_out if input is not None else residual)
+
+
+def silu_linear_w6ax(gate, up, wpk, N, abits=8, out=None):
+    """SiLU(gate) * up + quantize + W6Ax GEMM (fq_silu_linear_w6ax; down_proj after gate_up): one
+    launch at decode sizes, else fq_silu_mul_quantize + GEMM -- the same bits either way.  gate
+    and up as for silu_mul_quantize (e.g. the halves of a merged gate_up output)."""
+    for name, t in (("gate", gate), ("up", up)):
+        _need(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float16 and t.dim() == 2,
+              f"{name} must be a 2-D fp16 HIP tensor")
+        _need(t.stride(1) == 1, f"{name} rows must be contiguous")
+    _need(gate.shape == up.shape and gate.stride(0) == up.stride(0) and gate.device == up.device,
+          "gate and up must have one shape, row stride and device")
+    M, K = gate.shape
+    _k_ok(K)
+    dev = gate.device
+    _img_ok(wpk, N, K)
+    _need(wpk.device == dev, "the weight image must be on the activations' device")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    ld = gate.stride(0) if M > 1 else K
+    out = _out_ok(out, M, N, dev)
+    xq, xs = _act_scratch("fq_silu_linear_scratch_bytes", M, N, K, dev)
+    s = _stream(gate)
+    wbuf = workspace(dev, gemm_workspace_bytes(M, N, K), s.value)
+    _lib.call("fq_silu_linear_w6ax", _ptr(gate), _ptr(up), ld, M, N, K, abits, _ptr(wpk), _ptr(out), _ptr(xq),
+              _ptr(xs), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return out
+
+
 # ------------------------------------------------------------------------- reference layouts
 
 def _rows_ok(R):

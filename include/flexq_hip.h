@@ -149,6 +149,33 @@ fq_status fq_silu_mul_quantize(const uint16_t *gate, const uint16_t *up, int ld,
                                int abits, int8_t *xq, uint16_t *xs, uint16_t *act_out,
                                fq_stream_t stream);
 
+/* ---- producer + linear in one call: the decoder layer's three W6Ax linears that follow a producer
+ * (qkv and gate_up after the add-residual RMSNorm, down_proj after SiLU * up).  At decode sizes the
+ * producer runs inside the decode GEMM's prologue -- one launch instead of two: RMSNorm when
+ * M == 1 and K == 4096 (each of the 8 waves normalises and quantizes 4 of the 32 groups, the
+ * 512-thread producer's chunking), SiLU * up whenever fq_linear_w6ax would fuse its quantizer.
+ * Otherwise the producer kernel writes xq_buf / xs_buf (the *_scratch_bytes below) and the GEMM
+ * follows.  Outputs are bit-identical to fq_rmsnorm_quantize / fq_silu_mul_quantize followed by
+ * fq_gemm_w6ax, both ways.
+ * fq_rmsnorm_linear_w6ax: d = linear(RMSNorm(residual + input) codes); with input != NULL,
+ *   residual_out (NOT the residual itself: other workgroups are still reading it) receives
+ *   residual + input; with input == NULL the residual is only read.  Replaces the reference's
+ *   generalAddResidualT5LayerNormFlexQFusion + FLEXQGEMMWrapper::gemm pair
+ *   (LlamaContextDecoder.cc:576-592 then FfnLayer.cc:440-452).
+ * fq_silu_linear_w6ax: d = linear(codes of silu(gate) * up), gate / up rows of stride ld, K the
+ *   activation width (down_proj's input).  Replaces flexq_generic_activation + the down_proj GEMM
+ *   (FfnLayer.cc:521-558). */
+size_t fq_rmsnorm_linear_scratch_bytes(int M, int N, int K); /* M*K + 2*M*(K/128), or 0: fused */
+size_t fq_silu_linear_scratch_bytes(int M, int N, int K);
+fq_status fq_rmsnorm_linear_w6ax(const uint16_t *input, const uint16_t *residual, uint16_t *residual_out,
+                                 const uint16_t *gamma, float eps, int M, int N, int K, int abits,
+                                 const void *w_packed, uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf,
+                                 void *workspace, size_t workspace_bytes, fq_stream_t stream);
+fq_status fq_silu_linear_w6ax(const uint16_t *gate, const uint16_t *up, int ld, int M, int N, int K,
+                              int abits, const void *w_packed, uint16_t *d, int8_t *xq_buf,
+                              uint16_t *xs_buf, void *workspace, size_t workspace_bytes,
+                              fq_stream_t stream);
+
 /* ---- column-parallel decode with the all-gather in the GEMM epilogue -------
  * The north-star N-shard: rank p of P holds columns [col0, col0 + N) of a linear whose full width is
  * ld.  fq_linear_w6ax_gather computes this rank's columns exactly as fq_linear_w6ax does and stores

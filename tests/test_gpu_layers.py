@@ -264,3 +264,28 @@ def test_decoder_layer_two_processes(dev, weights, tmp_path):
         assert p_.exitcode == 0
     np.testing.assert_array_equal(res[0].numpy().view(np.uint16), res[1].numpy().view(np.uint16))
     np.testing.assert_array_equal(res[0].numpy().view(np.uint16), host(h).view(np.uint16))
+
+
+def test_run_layers_fused_producers_llama_width(dev):
+    """At the LLaMA-2-7B widths (H = 4096, F = 11008) run_layers takes the one-launch forms -- the
+    RMSNorm (+ residual add) inside qkv's and gate_up's decode GEMMs at M = 1, SiLU * up inside
+    down_proj's -- and must give the bits of the unfused layer calls (producer kernel, then GEMM)."""
+    from flexq_amd import ops
+    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear, run_layers
+    Hs, Fs = 4096, 11008
+    g = torch.Generator().manual_seed(31)
+    rnd = lambda n, k: (torch.randn((n, k), generator=g) / k ** 0.5).half().to(dev)  # noqa: E731
+    lin = lambda n, k, ab=6: W6Linear.from_fp16(rnd(n, k), ab)  # noqa: E731
+    ga = (1 + 0.1 * torch.randn(Hs, generator=g)).half().to(dev)
+    gf = (1 + 0.1 * torch.randn(Hs, generator=g)).half().to(dev)
+    ffn = FlexQFfn(lin(2 * Fs, Hs), lin(Hs, Fs, 8), gf)
+    L = FlexQDecoderLayer(lin(3 * Hs, Hs), lin(Hs, Hs), ffn, ga, lambda qkv: qkv[:, 2 * Hs:])
+    assert int(ops._lib.load().fq_rmsnorm_linear_scratch_bytes(1, 3 * Hs, Hs)) == 0  # fused at M = 1
+    assert int(ops._lib.load().fq_silu_linear_scratch_bytes(1, Hs, Fs)) == 0
+    for M in (1, 3):
+        x = torch.randn((M, Hs), generator=torch.Generator().manual_seed(40 + M)).half().to(dev)
+        h_ref = x.clone()
+        for _ in range(3):
+            L(h_ref)
+        h = run_layers([L, L, L], x.clone())
+        assert torch.equal(h.view(torch.int16), h_ref.view(torch.int16)), f"M = {M}"

@@ -154,3 +154,92 @@ def test_rmsnorm_within_one_ulp_of_reference_formula(ops, dev, M, K):
     got = host(normed).astype(np.float64)
     ulp = np.spacing(np.abs(ref16)).astype(np.float64)
     assert np.all(np.abs(got - ref) <= ulp), float((np.abs(got - ref) / ulp).max())
+
+
+def _image(ops, dev, N, K, seed):
+    w = (rng(seed).standard_normal((N, K)) / np.sqrt(K)).astype(np.float16)
+    return ops.quantize_pack_w6(to_dev(w, dev))[0]
+
+
+# (M, N, K): the fused one-launch forms (M = 1, K = 4096: qkv, gate_up, a narrow S = 1 width) and
+# the two-launch fallbacks (K != 4096, M > 1, a split-K shard width)
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (1, 12288, 4096), (1, 22016, 4096), (1, 2048, 4096),
+                                   (1, 256, 4096), (1, 4096, 2048), (4, 4096, 4096), (16, 1024, 8192)])
+@pytest.mark.parametrize("with_input", [True, False])
+def test_rmsnorm_linear_matches_producer_then_gemm(ops, dev, M, N, K, with_input):
+    """fq_rmsnorm_linear_w6ax (the norm inside the decode GEMM's prologue at M = 1, K = 4096)
+    against fq_rmsnorm_quantize + fq_gemm_w6ax: output and updated residual bit-identical, the
+    input residual untouched; and the output against the CPU oracle (norm + quantize + GEMM)."""
+    from common import assert_gemm_close
+    r = rng(M * 17 + N + K + with_input)
+    res = (r.standard_normal((M, K)) * 2.0).astype(np.float16)
+    inp = (r.standard_normal((M, K)) * 0.5).astype(np.float16) if with_input else None
+    gamma = (1.0 + 0.2 * r.standard_normal(K)).astype(np.float16)
+    res[0, :5] = [0.0, -0.0, 6e-8, -3e4, 3e4]
+    eps = 1e-5
+    wpk = _image(ops, dev, N, K, 5)
+    res_d, g_d = to_dev(res, dev), to_dev(gamma, dev)
+    inp_d = None if inp is None else to_dev(inp, dev)
+    fused_expected = M == 1 and K == 4096 and ops.gemm_workspace_bytes(M, N, K) == 0
+    assert (int(ops._lib.load().fq_rmsnorm_linear_scratch_bytes(M, N, K)) == 0) == fused_expected
+    y, h = ops.rmsnorm_linear_w6ax(res_d, g_d, wpk, N, 6, eps=eps, input=inp_d)
+    res2 = res_d.clone()
+    xq, xs = ops.rmsnorm_quantize(res2, g_d, 6, eps=eps, input=inp_d)
+    y2 = ops.gemm_w6ax(xq, xs, wpk, N, 6)
+    np.testing.assert_array_equal(hbits(host(y)), hbits(host(y2)), err_msg="output")
+    np.testing.assert_array_equal(hbits(host(h)), hbits(host(res2)), err_msg="updated residual")
+    np.testing.assert_array_equal(hbits(host(res_d)), hbits(res), err_msg="the residual must not change")
+    _, _, q_ref, xs_ref = oracle.rmsnorm_quantize(inp, res, gamma, eps, 6)
+    wq, ws = ops.unpack_w6(wpk, N, K)
+    ref, _, mag = oracle.gemm(q_ref, xs_ref, host(wq), host(ws))
+    assert_gemm_close(host(y), ref, mag, "rmsnorm_linear vs oracle")
+
+
+@pytest.mark.parametrize("M,N,K,bits", [(1, 4096, 11008, 8), (1, 4096, 14336, 8), (4, 4096, 11008, 8),
+                                        (16, 2048, 4096, 6), (32, 1024, 2048, 8), (1, 512, 11008, 8),
+                                        (64, 1024, 2048, 8), (1, 8192, 28672, 8)])
+def test_silu_linear_matches_producer_then_gemm(ops, dev, M, N, K, bits):
+    """fq_silu_linear_w6ax (SiLU * up inside the decode GEMM's prologue where the quantizer is fused)
+    against fq_silu_mul_quantize + fq_gemm_w6ax over a merged [gate | up] buffer: bit-identical;
+    and against the oracle GEMM of the producer's codes."""
+    from common import assert_gemm_close
+    r = rng(M * 5 + N + K)
+    gu = (r.standard_normal((M, 2 * K)) * 3.0).astype(np.float16)
+    gu[0, :4] = [0.0, -20.0, 20.0, -0.0]
+    gu_d = to_dev(gu, dev)
+    wpk = _image(ops, dev, N, K, 6)
+    y = ops.silu_linear_w6ax(gu_d[:, :K], gu_d[:, K:], wpk, N, bits)
+    xq, xs = ops.silu_mul_quantize(gu_d[:, :K], gu_d[:, K:], bits)
+    y2 = ops.gemm_w6ax(xq, xs, wpk, N, bits)
+    np.testing.assert_array_equal(hbits(host(y)), hbits(host(y2)))
+    wq, ws = ops.unpack_w6(wpk, N, K)
+    ref, _, mag = oracle.gemm(host(xq), host(xs), host(wq), host(ws))
+    assert_gemm_close(host(y), ref, mag, "silu_linear vs oracle")
+
+
+def test_fused_producer_linear_status_codes(ops, dev):
+    from flexq_amd import _lib
+    lib = _lib.load()
+    P = lambda n: torch.empty(n, dtype=torch.uint8, device=dev)  # noqa: E731
+    a, b, c, d = P(1 << 16), P(1 << 16), P(1 << 16), P(1 << 16)
+    wpk = _image(ops, dev, 64, 128, 7)
+    s = ops._stream(a)
+    ptr = ops._ptr
+    z = ctypes_size(0)
+    # residual_out == residual with an input: refused (other workgroups still read the residual)
+    assert lib.fq_rmsnorm_linear_w6ax(ptr(b), ptr(a), ptr(a), ptr(c), 1e-6, 1, 64, 128, 6, ptr(wpk), ptr(d),
+                                      None, None, None, z, s) == 2
+    assert lib.fq_rmsnorm_linear_w6ax(ptr(b), ptr(a), None, ptr(c), 1e-6, 1, 64, 128, 6, ptr(wpk), ptr(d),
+                                      None, None, None, z, s) == 1
+    assert lib.fq_rmsnorm_linear_w6ax(None, ptr(a), None, ptr(c), 1e-6, 1, 64, 100, 6, ptr(wpk), ptr(d),
+                                      None, None, None, z, s) == 2
+    assert lib.fq_silu_linear_w6ax(ptr(a), ptr(b), 64, 1, 64, 128, 8, ptr(wpk), ptr(d), None, None, None, z,
+                                   s) == 2  # ld < K
+    assert lib.fq_silu_linear_w6ax(ptr(a), ptr(b), 128, 1, 64, 128, 7, ptr(wpk), ptr(d), None, None, None, z,
+                                   s) == 3
+    torch.cuda.synchronize()
+
+
+def ctypes_size(n):
+    import ctypes
+    return ctypes.c_size_t(n)

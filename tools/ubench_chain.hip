@@ -28,6 +28,11 @@ __global__ __launch_bounds__(512) void k_empty(int *out) {
     if (threadIdx.x == 0 && out == nullptr) out[blockIdx.x] = 0;
 }
 
+__global__ __launch_bounds__(512) void k_empty_lds(int *out) {
+    extern __shared__ int sm[];
+    if (threadIdx.x == 0 && out == nullptr) out[blockIdx.x] = sm[0];
+}
+
 __global__ __launch_bounds__(512) void k_touch(const v4i *__restrict__ x, v4i *__restrict__ out) {
     const v4i v = x[threadIdx.x & 511];
     if (threadIdx.x == 0) out[blockIdx.x] = v;
@@ -95,6 +100,13 @@ int main(int argc, char **argv) {
         return best * 1000.f / R;  // us per launch
     };
     printf("empty   us/launch=%.2f\n", time_graph([&](int) { hipLaunchKernelGGL(k_empty, dim3(cus), dim3(512), 0, s, out); }));
+    for (int g : {1, 64, 256, 1024})
+        for (int t : {64, 256, 512})
+            printf("empty   grid=%4d threads=%3d us/launch=%.2f\n", g, t,
+                   time_graph([&](int) { hipLaunchKernelGGL(k_empty, dim3(g), dim3(t), 0, s, out); }));
+    for (int lds : {0, 32768, 98304})
+        printf("empty   grid=%4d threads=512 lds=%6d us/launch=%.2f\n", cus, lds,
+               time_graph([&](int) { hipLaunchKernelGGL(k_empty_lds, dim3(cus), dim3(512), lds, s, out); }));
     printf("touch   us/launch=%.2f\n", time_graph([&](int) { hipLaunchKernelGGL(k_touch, dim3(cus), dim3(512), 0, s, x, o4); }));
     for (long mb : sizes_mb) {
         if (!mb) continue;
