@@ -151,8 +151,19 @@ def _hip():
     raise RuntimeError("libamdhip64 not found")
 
 
-class _Handle:
-    SIZE = 64  # HIP_IPC_HANDLE_SIZE
+_IPC_HANDLE = []
+
+
+def _handle_type():
+    """hipIpcMemHandle_t (64 bytes), a Structure so that ctypes passes it BY VALUE to
+    hipIpcOpenMemHandle (a char array would decay to a pointer)."""
+    if not _IPC_HANDLE:
+        import ctypes
+
+        class IpcMemHandle(ctypes.Structure):
+            _fields_ = [("reserved", ctypes.c_char * 64)]  # HIP_IPC_HANDLE_SIZE
+        _IPC_HANDLE.append(IpcMemHandle)
+    return _IPC_HANDLE[0]
 
 
 def _ipc_export(t):
@@ -163,7 +174,7 @@ def _ipc_export(t):
     base, size = ctypes.c_void_p(), ctypes.c_size_t()
     if hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(t.data_ptr())) != 0:
         raise RuntimeError("hipMemGetAddressRange failed")
-    h = (ctypes.c_char * _Handle.SIZE)()
+    h = _handle_type()()
     if hip.hipIpcGetMemHandle(ctypes.byref(h), base) != 0:
         raise RuntimeError("hipIpcGetMemHandle failed (HSA_ENABLE_IPC_MODE_LEGACY=0 is required)")
     return bytes(h), t.data_ptr() - base.value
@@ -172,10 +183,12 @@ def _ipc_export(t):
 def _ipc_open(handle, offset):
     import ctypes
     hip = _hip()
-    h = (ctypes.c_char * _Handle.SIZE).from_buffer_copy(handle)
+    h = _handle_type().from_buffer_copy(handle)
     p = ctypes.c_void_p()
-    if hip.hipIpcOpenMemHandle(ctypes.byref(p), h, ctypes.c_uint(1)) != 0:  # hipIpcMemLazyEnablePeerAccess
-        raise RuntimeError("hipIpcOpenMemHandle failed")
+    hip.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), _handle_type(), ctypes.c_uint]
+    st = hip.hipIpcOpenMemHandle(ctypes.byref(p), h, ctypes.c_uint(1))  # hipIpcMemLazyEnablePeerAccess
+    if st != 0:
+        raise RuntimeError(f"hipIpcOpenMemHandle failed (hipError {st})")
     return p.value, p.value + offset
 
 
