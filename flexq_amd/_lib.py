@@ -99,7 +99,10 @@ def load():
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover - depends on the box
         raise FlexQExtensionError(f"failed to load {LIB_PATH}: {e}") from e
+    ab = LIB_PATH != os.path.join(_HERE, "libflexq_hip.so")  # an older A/B build may lack new entries
     for name, (args, res) in list(_SIGS.items()) + list(_STRUCT_SIGS.items()):
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

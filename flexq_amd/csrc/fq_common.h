@@ -200,18 +200,40 @@ __device__ __forceinline__ uint4 rms_apply8(uint4 r, uint4 g, float rs) {
                        half_clamp_f(__fmul_rn(__fmul_rn(hi_f(a[i]), rs), hi_f(gm[i]))));
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
-// act = half(silu(float(gate)) * float(up)), silu(v) = v / (1 + exp(-v)) with the hardware's fast
-// exp, as the reference's __expf                   (activation_kernels.cu:133, 300)
+// act = half(silu(float(gate)) * float(up)), silu(v) = v * rcp(1 + exp(-v)) with the hardware's
+// fast exp (the reference's __expf) and v_rcp_f32 (1 ulp) in place of the IEEE division
+// (activation_kernels.cu:133, 300): the fp32 silu is within ~2^-22 relative of the exact value, so
+// the fp16 product stays within one fp16 ulp of the exact one (the producers' tolerance), at a
+// fraction of the division's instructions.  Non-finite cases match the division: g = -inf gives
+// -inf * 0 = NaN (as -inf / inf), a large negative g gives -0.
 __device__ __forceinline__ uint4 silu_mul8(uint4 g4, uint4 u4) {
     const uint32_t g[4] = {g4.x, g4.y, g4.z, g4.w}, u[4] = {u4.x, u4.y, u4.z, u4.w};
     uint32_t o[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const float g0 = lo_f(g[i]), g1 = hi_f(g[i]);
-        const float s0 = g0 / (1.0f + __expf(-g0)), s1 = g1 / (1.0f + __expf(-g1));
+        const float s0 = g0 * __builtin_amdgcn_rcpf(1.0f + __expf(-g0));
+        const float s1 = g1 * __builtin_amdgcn_rcpf(1.0f + __expf(-g1));
         o[i] = pack_h2(__fmul_rn(s0, lo_f(u[i])), __fmul_rn(s1, hi_f(u[i])));
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Sum of a float over the 64 lanes of a wave, in a fixed tree: lane pairs, quads, 8- and 16-lane
+// halves on DPP (after each step every lane of a block holds the block's sum, so a mirror partner
+// is as good as the xor partner), then the four 16-lane rows as (r0 + r1) + (r2 + r3).  The same
+// bits as an xor butterfly over offsets 1, 2, 4, 8, 16, 32 (oracle/fq_oracle.c
+// fqo_rmsnorm_quantize); returns the wave-uniform total.
+__device__ __forceinline__ float wave_sum64(float v) {
+    v = v + dpp_f32<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+    v = v + dpp_f32<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+    v = v + dpp_f32<0x141>(v);  // row_half_mirror: the other quad of the 8
+    v = v + dpp_f32<0x140>(v);  // row_mirror: the other 8 of the 16
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 
 // arguments of a producer fused into the decode linear's prologue (fq_gemm.hip, PRO = 1 / 2)

@@ -220,6 +220,11 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
 //   PRO = 2: xh is the gate, `in` the up projection (row stride ldh): act = half(silu(gate) * up).
 // The arithmetic is fq_common.h's, shared with fq_producers.hip.
 // (DecodePro: fq_common.h)
+// development ablation of the fused producers (timing only, wrong results): 1 = no cross-lane /
+// cross-wave reduction, 2 = no input / gamma DMA, 4 = SiLU as a plain product, 8 = no up DMA
+#ifndef FQ_PRO_ABL
+#define FQ_PRO_ABL 0
+#endif
 
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
@@ -302,11 +307,11 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             const int j = M == 1 ? rg : rg / M, row = rg - j * M;
             const long off = (long)(ga + j) * FQ_GROUP + qsub * 8;
             __builtin_amdgcn_global_load_lds(xh + row * ldh + off, LDS_PTR(xh_st + c * 256), 16, 0, 0);
-            if (PRO == 1 && pro.in)
+            if (PRO == 1 && pro.in && !(FQ_PRO_ABL & 2))
                 __builtin_amdgcn_global_load_lds(pro.in + off, LDS_PTR(xh_st + xwb + c * 256), 16, 0, 0);
-            if (PRO == 1)
+            if (PRO == 1 && !(FQ_PRO_ABL & 2))
                 __builtin_amdgcn_global_load_lds(pro.gamma + off, LDS_PTR(xh_st + 2 * xwb + c * 256), 16, 0, 0);
-            if (PRO == 2)
+            if (PRO == 2 && !(FQ_PRO_ABL & 8))
                 __builtin_amdgcn_global_load_lds(pro.in + row * ldh + off, LDS_PTR(xh_st + xwb + c * 256), 16, 0, 0);
         }
     };
@@ -333,13 +338,15 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(raw0), "+v"(raw1)::"memory");
             }
             uint4 v0 = make_uint4(raw0[0], raw0[1], raw0[2], raw0[3]);
-            if (PRO == 2) v0 = silu_mul8(v0, make_uint4(up0[0], up0[1], up0[2], up0[3]));
+            if (PRO == 2 && (FQ_PRO_ABL & 4)) v0 = add_residual8(v0, make_uint4(up0[0], up0[1], up0[2], up0[3]));
+            else if (PRO == 2) v0 = silu_mul8(v0, make_uint4(up0[0], up0[1], up0[2], up0[3]));
             uint2 codes0;
             const uint16_t sh0 = quant_group16(v0, abits, codes0);
             x_store(rg, codes0, sh0);
             if (two) {
                 uint4 v1 = make_uint4(raw1[0], raw1[1], raw1[2], raw1[3]);
-                if (PRO == 2) v1 = silu_mul8(v1, make_uint4(up1[0], up1[1], up1[2], up1[3]));
+                if (PRO == 2 && (FQ_PRO_ABL & 4)) v1 = add_residual8(v1, make_uint4(up1[0], up1[1], up1[2], up1[3]));
+                else if (PRO == 2) v1 = silu_mul8(v1, make_uint4(up1[0], up1[1], up1[2], up1[3]));
                 uint2 codes1;
                 const uint16_t sh1 = quant_group16(v1, abits, codes1);
                 x_store(rg + 4, codes1, sh1);
@@ -432,17 +439,18 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
                 r = add_residual8(make_uint4(ii[0], ii[1], ii[2], ii[3]), r);
                 if (blockIdx.x == 0) *reinterpret_cast<uint4 *>(pro.res_out + 8 * (64 * wid + lane)) = r;
             }
-            float acc = sumsq8(r, 0.0f);
+            float acc = sumsq8(r, 0.0f), ss = acc;
+            if (!(FQ_PRO_ABL & 1)) {
+                acc = wave_sum64(acc);  // (fq_producers.hip's tree)
+                if (lane == 0) ds_write_b32(lds_addr(wsum) + 4 * wid, __float_as_uint(acc));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                v4i s0 = ds_read_b128(lds_addr(wsum)), s1 = ds_read_b128(lds_addr(wsum) + 16);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s0), "+v"(s1)::"memory");
+                ss = __int_as_float(s0[0]);
 #pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
-            if (lane == 0) ds_write_b32(lds_addr(wsum) + 4 * wid, __float_as_uint(acc));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            v4i s0 = ds_read_b128(lds_addr(wsum)), s1 = ds_read_b128(lds_addr(wsum) + 16);
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s0), "+v"(s1)::"memory");
-            float ss = __int_as_float(s0[0]);
-#pragma unroll
-            for (int w = 1; w < NW; w++) ss = ss + __int_as_float(w < 4 ? s0[w] : s1[w - 4]);
+                for (int w = 1; w < NW; w++) ss = ss + __int_as_float(w < 4 ? s0[w] : s1[w - 4]);
+            }
             uint2 codes;
             const uint16_t sh = quant_group16(rms_apply8(r, make_uint4(gg[0], gg[1], gg[2], gg[3]), rms_scale(ss, K, pro.eps)),
                                               abits, codes);

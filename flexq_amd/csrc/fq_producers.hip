@@ -25,12 +25,12 @@
 // Arithmetic (the oracle, oracle/fq_oracle.c fqo_rmsnorm_quantize / fqo_silu_mul, restates it):
 //   r      = half_clamp(float(input) + float(residual))              (layernorm_kernels.cu:1883)
 //   ss     = sum of float(r)^2: per thread fmaf over its chunks c*T + t in order, a 64-lane xor
-//            butterfly (32, 16, ..., 1), then the T/64 waves in order
+//            butterfly (1, 2, ..., 32; wave_sum64), then the T/64 waves in order
 //   rs     = 1 / sqrt(ss / K + eps)            (IEEE; the reference uses rsqrtf, :1890)
 //   normed = half_clamp((float(r) * rs) * float(gamma))              (:1898, two roundings)
 //   act    = half(silu(float(gate)) * float(up)), silu(v) = v / (1 + exp(-v))
 //            (activation_kernels.cu:133, 300; exp is the hardware's fast exp, as the
-//            reference's __expf)
+//            reference's __expf, and the division a v_rcp_f32 product: fq_common.h silu_mul8)
 // half_clamp = clamp_inf_for_half (reduce_kernel_utils.cuh:357-361): clamp to +-(65504 - 1000),
 // then round to fp16.
 #include "fq_common.h"
@@ -78,8 +78,7 @@ __global__ __launch_bounds__(T) void fq_rmsnorm_quant_kernel(const uint16_t *__r
             acc = sumsq8(res, acc);
         }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+    acc = wave_sum64(acc);
     if (lane == 0) wsum[wid] = acc;
     __syncthreads();
     float ss = wsum[0];

@@ -406,7 +406,7 @@ static uint16_t half_clamp(float v) {
  * kernel (flexq_amd/csrc/fq_producers.hip), so that the comparison is bit-exact:
  *   r = half_clamp(float(in) + float(res))                                  (:1883)
  *   ss: thread t of T sums fmaf(v, v, acc) over its chunks c*T+t of 8 values in order; a 64-lane
- *       xor butterfly (32, 16, ..., 1); the T/64 waves added in order.  T = 256, 512 or 1024 as
+ *       xor butterfly (1, 2, ..., 32: fq_common.h wave_sum64); the T/64 waves added in order.  T = 256, 512 or 1024 as
  *       the row has <= 256, <= 512 or more chunks (the kernel's workgroup size)
  *   rs = 1 / sqrt(ss / K + eps)        (the reference: rsqrtf, :1890)
  *   normed = half_clamp((float(r) * rs) * float(gamma))                     (:1898)
@@ -436,7 +436,7 @@ int fqo_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const uint16
         for (int w = 0; w < T / 64; w++) {
             float lane[64];
             for (int l = 0; l < 64; l++) lane[l] = acc[64 * w + l];
-            for (int off = 32; off >= 1; off >>= 1) {
+            for (int off = 1; off <= 32; off <<= 1) {
                 float nxt[64];
                 for (int l = 0; l < 64; l++) nxt[l] = lane[l] + lane[l ^ off];
                 memcpy(lane, nxt, sizeof(lane));
