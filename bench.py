@@ -585,16 +585,32 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
     return res
 
 
-def optional(res, key, fn):
+def optional(res, key, fn, ctx=None, need_bytes=0):
     """An optional section of the line (the replicas, C4, the decoder layers): an exception there
-    is recorded under `key` instead of costing the headline line.  The sections run the same code
-    on every rank, so a deterministic failure is skipped by all ranks alike."""
+    is recorded under `key` instead of costing the headline line.  With several ranks the ranks
+    agree before (every rank must have `need_bytes` of device memory free -- all ranks' share
+    under --share-gpu -- or the section is skipped on all) and after (a failure on any rank is a
+    failure on every rank), so no rank goes on to the next section's collectives alone."""
+    multi = ctx is not None and ctx.world > 1
+    if need_bytes:
+        free = torch.cuda.mem_get_info(ctx.dev if ctx is not None else None)[0]
+        want = 1.15 * need_bytes * (ctx.world if multi and ctx.staged else 1)
+        short = 1.0 if free < want else 0.0
+        if (ctx.max_over_ranks(short) if multi else short) > 0:
+            res[key] = {"skipped": f"needs ~{want / 1e9:.1f} GB of free device memory per GPU "
+                                   f"({free / 1e9:.1f} GB free on this rank)"}
+            print(f"[bench] optional section {key} skipped: {res[key]['skipped']}", file=sys.stderr, flush=True)
+            return
+    err = None
     try:
-        res[key] = fn()
+        out = fn()
     except Exception as e:  # noqa: BLE001
-        res[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        err = f"{type(e).__name__}: {e}"[:500]
         print(f"[bench] optional section {key} failed: {e}", file=sys.stderr, flush=True)
         torch.cuda.empty_cache()
+    if multi and ctx.max_over_ranks(1.0 if err else 0.0) > 0 and err is None:
+        err = "failed on another rank"
+    res[key] = {"error": err} if err else out
 
 
 def main():
@@ -787,7 +803,8 @@ def main():
                         "value": round(world * flops_step * a.steps / el_dp / 1e12, 4),
                         "tok_per_s": round(world * M * a.steps / el_dp, 2),
                         "ms_per_step": round(el_dp / a.steps * 1e3, 4)}
-            optional(res, "replicas", replicas)
+            need = cfg[0] * sum(ops.packed_w_bytes(N, K) for (_, N, K, _) in launch_lins)
+            optional(res, "replicas", replicas, ctx, need_bytes=need)
         if not a.no_peer and M <= 32:  # the all-gather fused into the GEMM epilogue
             def tp_peer(c):
                 rp = measure_tp(ctx, c, merge, tp, max(2, a.steps // 2), max(1, a.warmup // 2), peer=True)
@@ -799,9 +816,9 @@ def main():
                         "ms_per_step": round(rp["ms_per_step"], 4),
                         "gemm_only_ms_per_step": round(rp["gemm_only_ms_per_step"], 4),
                         "finite": rp["finite"], "graph": rp["graph"]}
-            optional(res, "tp_peer_gather", lambda: tp_peer(cfg))
+            optional(res, "tp_peer_gather", lambda: tp_peer(cfg), ctx)
             if not a.no_c4 and a.config != "llama2-70b-m1":
-                optional(res, "c4_llama2_70b_tp_peer_gather", lambda: tp_peer(CONFIGS["llama2-70b-m1"]))
+                optional(res, "c4_llama2_70b_tp_peer_gather", lambda: tp_peer(CONFIGS["llama2-70b-m1"]), ctx)
         if not a.no_c4 and a.config != "llama2-70b-m1" and not prefill:
             def c4_tp():
                 c4 = CONFIGS["llama2-70b-m1"]
@@ -814,7 +831,7 @@ def main():
                     **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in rc.items()
                        if k not in ("elapsed", "flops_step")},
                     "hbm_frac_per_rank": round(rc["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
-            optional(res, "c4_llama2_70b_tp", c4_tp)
+            optional(res, "c4_llama2_70b_tp", c4_tp, ctx)
     if not a.no_layers and not prefill and a.config.startswith("llama2-7b"):
         optional(res, "decoder_layers_e2e", lambda: {
             "what": f"LLaMA-2-7B decoder layers end to end (32 layers; RMSNorm, qkv, o, gate_up, SiLU*up, down, "
@@ -822,7 +839,7 @@ def main():
                     f"(row-parallel o/down + one all-reduce each), W6A6 (down W6A8) engine vs fp16 torch "
                     f"(F.rms_norm, hipBLASLt F.linear, F.silu), one HIP graph each; README.md:193's comparison",
             "tp": world,
-            **{f"M{m}": decoder_layers_e2e(ctx, m) for m in (1, 16)}})
+            **{f"M{m}": decoder_layers_e2e(ctx, m) for m in (1, 16)}}, ctx)
     if world == 1 and not a.no_calibrate:
         res["roofline"]["peak_measured"] = calibrate_peaks(dev)
         pm = res["roofline"]["peak_measured"]
