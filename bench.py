@@ -488,7 +488,14 @@ def measure_tp(ctx, cfg, merge, tp, steps, warmup, peer=False):
     stack = build_stack(cfg, ctx.rank, tp, ctx.dev, merge, peer=peer)
     use_graph = not ctx.a.no_graph and (peer or not ctx.staged)
     replay = ctx.prepare(lambda: run_step(stack, M, tp, staged=ctx.staged), use_graph)
+
+    def peer_check(when):  # a timed-out peer wait on any rank fails the section on every rank
+        pgs = {id(p["pg"]): p["pg"] for _, p in linears(stack) if "pg" in p}.values() if peer else ()
+        if peer and ctx.max_over_ranks(float(any(pg.error() for pg in pgs))) > 0:
+            raise RuntimeError(f"peer-store gather: a wait timed out ({when})")
+    peer_check("warm-up")
     elapsed, _ = ctx.timed(replay, steps, warmup)
+    peer_check("timed steps")
     n_lin = layers * len(launch_lins)
     gemm_step, per_launch = ctx.graph_time(lambda: run_step(stack, M, tp, gather=False), n_lin,
                                            ctx.a.roofline_reps)

@@ -604,14 +604,16 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
 
 // Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q
 // polls rank q's flag with system-scope loads, sleeping between polls), then acquire and advance
-// the generation.  Bounded: after ~4 s the error word is set and the kernel returns (results are
-// then undefined, never a hang).
+// the generation.  Bounded: after ~1 s the error word is set and the kernel returns (results are
+// then undefined, never a hang); once the error word is set every later wait returns at once, so a
+// broken peer path costs one timeout, not one per call.
 __global__ __launch_bounds__(64) void fq_gather_wait_kernel(const fq_gather *__restrict__ gat, uint32_t *__restrict__ err) {
     const int lane = threadIdx.x;
+    if (err && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     const uint32_t target = __hip_atomic_load(gat->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const uint32_t *mine = gat->flags[gat->rank];
     bool ok = lane >= gat->P;
-    for (int spin = 0; spin < (1 << 22); spin++) {  // ~4 s at ~1 us per poll
+    for (int spin = 0; spin < (1 << 20); spin++) {  // ~1 s at ~1 us per poll
         if (!ok) ok = __hip_atomic_load(mine + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target;
         if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
         __builtin_amdgcn_s_sleep(8);

@@ -188,7 +188,8 @@ fq_status fq_silu_linear_w6ax(const uint16_t *gate, const uint16_t *up, int ld, 
  * Use two gather buffers alternately (linear j writes buffer j % 2): a rank can then run at most
  * one linear ahead of any other without overwriting an input still being read.  The struct lives
  * in device memory; done and gen are this rank's own words, zeroed once.  The wait is bounded
- * (~4 s): on timeout *err is set to 1 and the results are undefined (never a hang).
+ * (~1 s): on timeout *err is set to 1 and the results are undefined (never a hang); while *err is
+ * set, fq_gather_wait returns at once.
  * M <= 32, N % 16 == 0, P <= FQ_GATHER_MAX_RANKS. */
 #define FQ_GATHER_MAX_RANKS 8
 typedef struct fq_gather {

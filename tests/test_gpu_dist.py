@@ -120,3 +120,37 @@ def test_peer_store_gather_matches_all_gather(dev, world):
             for i, (g, w) in enumerate(zip(got, want)):
                 np.testing.assert_array_equal(g.view(np.uint16), w.view(np.uint16), err_msg=f"rank {r} call {i}")
             np.testing.assert_array_equal(got[-1].view(np.uint16), res[0][(M, N, K, abits)][0][-1].view(np.uint16))
+
+
+def test_gather_wait_times_out_once_then_fails_fast(dev):
+    """fq_gather_wait is bounded: with a flag that never arrives it sets the error word after about
+    a second and returns (never a hang), and every later wait with the error word set returns at
+    once (a broken peer path costs one timeout, not one per linear)."""
+    import ctypes
+    import time
+    from flexq_amd import _lib, ops
+    P8, I4 = ctypes.c_uint64 * 8, ctypes.c_int32 * 4
+
+    class Desc(ctypes.Structure):  # fq_gather (include/flexq_hip.h)
+        _fields_ = [("out", P8), ("flags", P8), ("done", ctypes.c_uint64), ("gen", ctypes.c_uint64), ("ints", I4)]
+    buf = torch.zeros((1, 16), dtype=torch.float16, device=dev)
+    flags = torch.zeros(8, dtype=torch.int32, device=dev)  # never raised
+    state = torch.zeros(2, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    d = Desc()
+    d.out[0], d.flags[0] = buf.data_ptr(), flags.data_ptr()
+    d.done, d.gen = state.data_ptr(), state.data_ptr() + 4
+    d.ints = I4(1, 0, 0, 16)
+    desc = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).to(dev)
+    s = ops._stream(buf)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    _lib.call("fq_gather_wait", ops._ptr(desc), ops._ptr(err), s)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    assert int(err.item()) == 1 and int(state[1].item()) == 0  # timed out, generation not advanced
+    assert 0.05 < t1 - t0 < 30, t1 - t0
+    for _ in range(20):
+        _lib.call("fq_gather_wait", ops._ptr(desc), ops._ptr(err), s)
+    torch.cuda.synchronize()
+    assert time.time() - t1 < 0.5 * (t1 - t0) + 0.05, "waits with the error word set must return at once"
