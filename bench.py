@@ -516,6 +516,56 @@ def measure_tp(ctx, cfg, merge, tp, steps, warmup, peer=False):
                 launches_per_step=n_lin, fused_launches=all(fused.values()), graph=use_graph, finite=finite)
 
 
+def measure_single(ctx, name, merge, steps, warmup):
+    """Another BASELINE config on this one GPU, measured in the same run as the headline (C3's
+    batch-16 step, C5's prefill step): the whole step as one HIP graph of its launches (quantize +
+    GEMM per linear where they are separate), and for prefill the GEMM launches alone on
+    pre-quantized codes (the MFMA roofline)."""
+    cfg = CONFIGS[name]
+    layers, M, lins, desc = cfg
+    launch_lins = launch_list(lins, merge)
+    n_lin = layers * len(launch_lins)
+    stack = build_stack(cfg, ctx.rank, 1, ctx.dev, merge)
+    replay = ctx.prepare(lambda: run_step(stack, M, 1), not ctx.a.no_graph)
+    elapsed, ev_s = ctx.timed(replay, steps, warmup)
+    flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)
+    out = {"what": f"BASELINE config: {desc}, the dependent linear stack of every layer, one HIP graph",
+           "ms_per_step": round(elapsed / steps * 1e3, 4),
+           "value": round(flops_step * steps / elapsed / 1e12, 4), "unit": "TFLOPS-equiv",
+           "tok_per_s": round(M * steps / elapsed, 2), "steps": steps, "warmup": warmup,
+           "finite": bool(torch.isfinite(linears(stack)[-1][1]["out"].float()).all().item())}
+    if M > PREFILL_M:
+        codes = {}
+        for nm, p in linears(stack):
+            if nm not in codes:
+                codes[nm] = ops.quantize_act(p["x"], p["abits"])
+
+        def gemms():
+            for nm, p in linears(stack):
+                ops.gemm_w6ax(codes[nm][0], codes[nm][1], p["pk"], p["Nl"], p["abits"], out=p["out"])
+        _, per_gemm_s = ctx.graph_time(gemms, n_lin, 2)
+        ops_launch = layers * sum(2.0 * M * N * K for (_, N, K, _) in launch_lins) / n_lin
+        ach = ops_launch / per_gemm_s / 1e12
+        out["roofline"] = {"kernel": "fq_gemm_prefill_big_kernel" if M >= 2048 else "fq_gemm_prefill_kernel",
+                           "bound": "mfma", "achieved": round(ach, 1), "peak": I8_MFMA_PEAK_TOPS,
+                           "unit": "TFLOP/s", "frac": round(ach / I8_MFMA_PEAK_TOPS, 4),
+                           "per_launch_us": round(per_gemm_s * 1e6, 3)}
+        del codes
+    else:
+        per_launch = ev_s / (steps * n_lin)
+        fused = {(N, K): ops.act_scratch_bytes(M, N, K) == 0 for (_, N, K, _) in launch_lins}
+        bytes_launch = layers * sum(alg_bytes(M, N, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins) / n_lin
+        out["roofline"] = {"kernel": "fq_gemm_decode_kernel" + ("<FUSE>" if all(fused.values()) else
+                                                                 " + the separate quantize launch"),
+                           "bound": "hbm", "achieved": round(bytes_launch / per_launch / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(bytes_launch / per_launch / 1e9 / HBM_PEAK_GBS, 4),
+                           "per_launch_us_incl_quantize": round(per_launch * 1e6, 3)}
+    del stack, replay
+    torch.cuda.empty_cache()
+    return out
+
+
 def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
     """SURVEY.md §8(f)3 / README.md:193: LLaMA-2-7B decoder layers end to end (norms, SiLU*up,
     the four linears, residuals; the attention core is out of scope and stands in as ctx = v,
@@ -643,6 +693,8 @@ def main():
                     help="N > 1, tp: skip the peer-store gather variant (all-gather fused into the GEMM epilogue)")
     ap.add_argument("--no-c4", action="store_true",
                     help="N > 1: skip the LLaMA-2-70B column-parallel measurement (BASELINE config C4)")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="N = 1: skip the C3 (batch 16) and C5 (prefill) steps measured beside the headline")
     ap.add_argument("--no-layers", action="store_true",
                     help="skip the end-to-end decoder-layer comparison against fp16 (M = 1 and 16)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -839,6 +891,11 @@ def main():
                        if k not in ("elapsed", "flops_step")},
                     "hbm_frac_per_rank": round(rc["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
             optional(res, "c4_llama2_70b_tp", c4_tp, ctx)
+    if world == 1 and not a.no_extra_configs:  # the other single-GPU BASELINE configs, same run
+        for key, name, st, wu in (("c3_llama2_7b_m16", "llama2-7b-m16", 10, 3),
+                                  ("c5_llama3_8b_prefill", "llama3-8b-prefill", 2, 1)):
+            if name != a.config:
+                optional(res, key, lambda name=name, st=st, wu=wu: measure_single(ctx, name, merge, st, wu), ctx)
     if not a.no_layers and not prefill and a.config.startswith("llama2-7b"):
         optional(res, "decoder_layers_e2e", lambda: {
             "what": f"LLaMA-2-7B decoder layers end to end (32 layers; RMSNorm, qkv, o, gate_up, SiLU*up, down, "
