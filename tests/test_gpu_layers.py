@@ -223,10 +223,13 @@ def _mp_worker(rank, world, port, out_dir, x, ga, gf, q):
     from flexq_amd.layers import FlexQDecoderLayer
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
+        from flexq_amd.layers import run_layers
         L = FlexQDecoderLayer.from_dir(out_dir, 0, ga, gf, _attn_stand_in, rank=rank, device="cuda:0")
         h = L(x.to("cuda:0").clone())
+        h2 = L(h.clone())  # two layers one by one ...
+        hr = run_layers([L, L], x.to("cuda:0").clone())  # ... and through run_layers' fused forms
         torch.cuda.synchronize()
-        q.put((rank, h.cpu()))
+        q.put((rank, h.cpu(), h2.cpu(), hr.cpu()))
     finally:
         dist.destroy_process_group()
 
@@ -258,12 +261,17 @@ def test_decoder_layer_two_processes(dev, weights, tmp_path):
     procs = [ctx.Process(target=_mp_worker, args=(r, 2, port, out, x, ga, w["gamma"], q)) for r in range(2)]
     for p_ in procs:
         p_.start()
-    res = dict(q.get(timeout=100) for _ in range(2))
+    res = {}
+    for _ in range(2):
+        r, *outs = q.get(timeout=100)
+        res[r] = [o.numpy().view(np.uint16) for o in outs]
     for p_ in procs:
         p_.join(timeout=60)
         assert p_.exitcode == 0
-    np.testing.assert_array_equal(res[0].numpy().view(np.uint16), res[1].numpy().view(np.uint16))
-    np.testing.assert_array_equal(res[0].numpy().view(np.uint16), host(h).view(np.uint16))
+    for k in range(3):
+        np.testing.assert_array_equal(res[0][k], res[1][k])
+    np.testing.assert_array_equal(res[0][0], host(h).view(np.uint16))
+    np.testing.assert_array_equal(res[0][2], res[0][1])  # run_layers == layer by layer, with all-reduces
 
 
 def test_run_layers_fused_producers_llama_width(dev):
