@@ -499,7 +499,9 @@ def measure_tp(ctx, cfg, merge, tp, steps, warmup, peer=False):
     n_lin = layers * len(launch_lins)
     gemm_step, per_launch = ctx.graph_time(lambda: run_step(stack, M, tp, gather=False), n_lin,
                                            ctx.a.roofline_reps)
-    finite = bool(torch.isfinite(linears(stack)[-1][1]["full"].float()).all().item())
+    last_full = linears(stack)[-1][1]["full"]
+    finite = bool(torch.isfinite(last_full.float()).all().item())
+    final = last_full.view(-1)[:M * linears(stack)[-1][1]["N"]].cpu().numpy().copy()  # the step's output
     gemm_ms = ctx.max_over_ranks(gemm_step) * 1e3
     per_launch = ctx.max_over_ranks(per_launch)
     fused = {(N, K): ops.act_scratch_bytes(M, N // tp, K) == 0 for (_, N, K, _) in launch_lins}
@@ -513,7 +515,8 @@ def measure_tp(ctx, cfg, merge, tp, steps, warmup, peer=False):
                 hbm_GBps_per_rank=bytes_launch / per_launch / 1e9,
                 allgather_bytes_per_step_per_rank=int(layers * sum(2 * M * (N // tp) * (tp - 1)
                                                                    for (_, N, K, _) in launch_lins)),
-                launches_per_step=n_lin, fused_launches=all(fused.values()), graph=use_graph, finite=finite)
+                launches_per_step=n_lin, fused_launches=all(fused.values()), graph=use_graph, finite=finite,
+                final=final)
 
 
 def measure_single(ctx, name, merge, steps, warmup):
@@ -732,6 +735,20 @@ def main():
 
     if tp > 1:
         r = measure_tp(ctx, cfg, merge, tp, a.steps, a.warmup)
+        # The column-parallel step's all-gather has two implementations: RCCL's all_gather and the
+        # peer-store gather fused into the GEMM epilogue.  Both run; the peer one is
+        # taken for `value` only when every rank's step output is bit-identical to the RCCL run's,
+        # no wait timed out and it is faster (never in the --share-gpu rehearsal).
+        gather_impl, r_rccl, peer_sec = "rccl all_gather_into_tensor", r, {}
+        if not a.no_peer and M <= PREFILL_M:
+            optional(peer_sec, "p", lambda: measure_tp(ctx, cfg, merge, tp, a.steps, a.warmup, peer=True), ctx)
+            rp = peer_sec["p"]
+            if "final" in rp:
+                bad = 0.0 if (rp["finite"] and np.array_equal(rp["final"].view(np.uint16),
+                                                              r["final"].view(np.uint16))) else 1.0
+                rp["bit_identical_to_rccl"] = ctx.max_over_ranks(bad) == 0.0
+                if rp["bit_identical_to_rccl"] and rp["elapsed"] < r["elapsed"] and not staged:
+                    r, gather_impl = rp, "peer-store gather in the GEMM epilogue (fq_linear_w6ax_gather)"
         elapsed = r["elapsed"]
         value = flops_step * a.steps / elapsed / 1e12
         tok_s = M * a.steps / elapsed
@@ -796,8 +813,8 @@ def main():
             "workload": desc + ", dependent linear stack of every decoder layer per step",
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
-            "parallelism": (f"tp{world}: every linear column-parallel (N/{world} rows per rank) + one RCCL "
-                            f"all-gather of its fp16 output per linear" if tp > 1 else
+            "parallelism": (f"tp{world}: every linear column-parallel (N/{world} rows per rank) + one "
+                            f"all-gather of its fp16 output per linear ({gather_impl})" if tp > 1 else
                             f"dp{world}: independent replicas, one token stream per GPU, no data-path collective"),
             "graph": use_graph,
             "launches_per_layer": [[name, N // tp, K, ab] for (name, N, K, ab) in launch_lins],
@@ -848,7 +865,9 @@ def main():
         }
     if tp > 1:
         res["tp"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()
-                     if k not in ("elapsed", "flops_step", "finite")}
+                     if k not in ("elapsed", "flops_step", "finite", "final")}
+        res["tp"]["gather"] = gather_impl
+        res["tp"]["rccl_ms_per_step"] = round(r_rccl["ms_per_step"], 4)
         res["tp"]["hbm_frac_per_rank"] = round(r["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)
         if not a.no_replicas:  # the same model as independent replicas, one token stream per GPU
             def replicas():
@@ -875,7 +894,18 @@ def main():
                         "ms_per_step": round(rp["ms_per_step"], 4),
                         "gemm_only_ms_per_step": round(rp["gemm_only_ms_per_step"], 4),
                         "finite": rp["finite"], "graph": rp["graph"]}
-            optional(res, "tp_peer_gather", lambda: tp_peer(cfg), ctx)
+            rp = peer_sec.get("p")
+            if rp is not None and "final" in rp:
+                res["tp_peer_gather"] = {
+                    "what": "the same column-parallel stack, each all-gather fused into its GEMM's epilogue: peer "
+                            "stores into IPC-mapped gather buffers + one wait launch per linear "
+                            "(fq_linear_w6ax_gather / fq_gather_wait) instead of an RCCL all_gather",
+                    "value": round(rp["flops_step"] / (rp["ms_per_step"] / 1e3) / 1e12, 4), "unit": "TFLOPS-equiv",
+                    "tok_per_s": round(M * 1e3 / rp["ms_per_step"], 2), "ms_per_step": round(rp["ms_per_step"], 4),
+                    "gemm_only_ms_per_step": round(rp["gemm_only_ms_per_step"], 4), "finite": rp["finite"],
+                    "bit_identical_to_rccl": rp["bit_identical_to_rccl"], "graph": rp["graph"]}
+            elif rp is not None:
+                res["tp_peer_gather"] = rp
             if not a.no_c4 and a.config != "llama2-70b-m1":
                 optional(res, "c4_llama2_70b_tp_peer_gather", lambda: tp_peer(CONFIGS["llama2-70b-m1"]), ctx)
         if not a.no_c4 and a.config != "llama2-70b-m1" and not prefill:
@@ -888,7 +918,7 @@ def main():
                     "value": round(rc["flops_step"] / (rc["ms_per_step"] / 1e3) / 1e12, 4),
                     "unit": "TFLOPS-equiv", "tok_per_s": round(1e3 / rc["ms_per_step"], 2),
                     **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in rc.items()
-                       if k not in ("elapsed", "flops_step")},
+                       if k not in ("elapsed", "flops_step", "final")},
                     "hbm_frac_per_rank": round(rc["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
             optional(res, "c4_llama2_70b_tp", c4_tp, ctx)
     if world == 1 and not a.no_extra_configs:  # the other single-GPU BASELINE configs, same run
