@@ -161,7 +161,7 @@ __device__ __forceinline__ void gather_publish(const fq_gather *__restrict__ gat
 // in the poller's XCD L2 and never see another XCD's atomic -- DESIGN.md §8, the round-2 tail-split
 // hang), followed by ONE agent acquire, with a bounded spin that ends in a printf of the ticket
 // value and __builtin_trap() (MI355X_MICROARCH.md "Valid forms", Consumer bullet).
-template <int NW>
+template <int NW, bool GAT>
 __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N, int Npad, int EM, int t0,
                                                     int tstep, float *__restrict__ slabs,
                                                     uint32_t *__restrict__ tickets, uint16_t *__restrict__ d,
@@ -176,11 +176,11 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
         flag[threadIdx.x] = last;
     }
     __syncthreads();  // (the flag is read behind this barrier: the slab loads cannot move above it)
-    const int GP = gat ? gat->P : 0;  // (gather: two adjacent columns per thread, 4-byte stores)
+    const int GP = GAT ? gat->P : 0;  // (gather: two adjacent columns per thread, 4-byte stores)
     for (int it = 0; it < nit; it++) {
         if (!flag[it]) continue;  // workgroup-uniform
         const int t = t0 + it * tstep;
-        if (gat) {
+        if (GAT) {
             for (int e = 2 * threadIdx.x; e < EM; e += 2 * NW * 64) {
                 const int row = e >> 4, nn = 16 * t + (e & 15);
                 float v0 = 0.f, v1 = 0.f;
@@ -229,12 +229,12 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
-template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0>
-__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0, bool GAT = false>
+__device__ __forceinline__ void decode_body(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
     float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir,
-    int NCH, const fq_gather *__restrict__ gat, const DecodePro pro) {
+    int NCH, const fq_gather *__restrict__ gat, const DecodePro &pro) {
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
     // second serial round trip before the first DMA; tools/stamps.py).
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
-            if (S == 1 && gat) {  // peer-store gather: two adjacent columns per thread
+            if (GAT && S == 1) {  // peer-store gather: two adjacent columns per thread
                 for (int e = 2 * threadIdx.x; e < (rs + 1) * EM; e += 2 * NW * 64) {
                     const int k = e / EM, ee = e - k * EM;
                     float v0 = 0.f, v1 = 0.f;
@@ -597,10 +597,41 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
         }
     }
     FQ_STAMP(3);
-    if (S > 1 && !(ABL & 4)) decode_splitk_fixup<NW>(nit, S, M, N, Npad, EM, t0, tstep, slabs, tickets, d, flag, gat);
-    FQ_STAMP(4);
-    if (gat) gather_publish(gat);
+    // GAT is a separate instantiation: the gather's branches and publish step cost the plain
+    // kernel ~3.5 % per launch when they are only runtime-dead (A/B over round 3's builds,
+    // tools/ab_bisect.sh)
+    if (!GAT) {
+        if (S == 1 || (ABL & 4)) return;
+        decode_splitk_fixup<NW, false>(nit, S, M, N, Npad, EM, t0, tstep, slabs, tickets, d, flag, nullptr);
+        FQ_STAMP(4);
+        return;
+    }
+    if (S > 1 && !(ABL & 4)) decode_splitk_fixup<NW, true>(nit, S, M, N, Npad, EM, t0, tstep, slabs, tickets, d, flag, gat);
+    gather_publish(gat);
 }
+
+// The kernels around decode_body.  The plain one keeps the short argument list: its explicit
+// arguments and the hidden block count it reads stay within the first 128 bytes of the kernarg
+// segment -- 40 more bytes of (unused) arguments cost the plain launch ~2.5 % (A/B/A/B,
+// tools/ab_karg.sh) -- and only the peer-store gather and the fused producers take the long one.
+#define FQ_DECODE_ARGS                                                                                              \
+    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,      \
+        const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d,                          \
+        int32_t *__restrict__ acc_dbg, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW,    \
+        int RC, int xwin, int iq, int ir, int NCH
+#define FQ_DECODE_PASS xq, xs, xh, abits, wpk, Mall, N, K, d, acc_dbg, slabs, tickets, S, IPW, RC, xwin, iq, ir, NCH
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(FQ_DECODE_ARGS) {
+    decode_body<MT, XS, SS, FUSE, DBG, ABL, CH, 0, false>(FQ_DECODE_PASS, nullptr, DecodePro{});
+}
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int PRO, bool GAT>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ext_kernel(FQ_DECODE_ARGS,
+                                                                                   const fq_gather *__restrict__ gat,
+                                                                                   const DecodePro pro) {
+    decode_body<MT, XS, SS, FUSE, DBG, 0, false, PRO, GAT>(FQ_DECODE_PASS, gat, pro);
+}
+#undef FQ_DECODE_ARGS
+#undef FQ_DECODE_PASS
 
 // Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q
 // polls rank q's flag with system-scope loads, sleeping between polls), then acquire and advance
@@ -1523,7 +1554,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
                            a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
                            slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),              \
-                           p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat, a.pro);                                 \
+                           p.NT * p.S % (p.grid / p.NCH), p.NCH);                                               \
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
@@ -1531,10 +1562,25 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 #undef FQ_ABL
     }
 #endif
-    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH, PRO>), grid, block, lds, stream, a.xq, a.xs,
+    if constexpr (!CH) {
+        if (PRO != 0 || a.gat) {  // the fused producers and the peer-store gather: the long argument list
+            if (a.gat)
+                hipLaunchKernelGGL((fq_gemm_decode_ext_kernel<MT, XS, SS, FUSE, DBG, 0, true>), grid, block, lds,
+                                   stream, a.xq, a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d,
+                                   a.acc_dbg, slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),
+                                   p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat, a.pro);
+            else
+                hipLaunchKernelGGL((fq_gemm_decode_ext_kernel<MT, XS, SS, FUSE, DBG, PRO, false>), grid, block, lds,
+                                   stream, a.xq, a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d,
+                                   a.acc_dbg, slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),
+                                   p.NT * p.S % (p.grid / p.NCH), p.NCH, nullptr, a.pro);
+            FQ_LAUNCH_CHECK();
+            return FQ_OK;
+        }
+    }
+    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH>), grid, block, lds, stream, a.xq, a.xs,
                        a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S,
-                       p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH,
-                       a.gat, a.pro);
+                       p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
