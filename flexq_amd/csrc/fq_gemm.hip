@@ -613,7 +613,8 @@ __device__ __forceinline__ void decode_body(
 // The kernels around decode_body.  The plain one keeps the short argument list: its explicit
 // arguments and the hidden block count it reads stay within the first 128 bytes of the kernarg
 // segment -- 40 more bytes of (unused) arguments cost the plain launch ~2.5 % (A/B/A/B,
-// tools/ab_karg.sh) -- and only the peer-store gather and the fused producers take the long one.
+// tools/ab_karg.sh) -- and only the peer-store gather takes the long one (the fused producers
+// have their own short list, fq_gemm_decode_pro_kernel).
 #define FQ_DECODE_ARGS                                                                                              \
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,      \
         const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d,                          \
@@ -632,6 +633,18 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ext_kern
 }
 #undef FQ_DECODE_ARGS
 #undef FQ_DECODE_PASS
+// The fused producers' kernel: the plain argument list's length (hidden arguments at 0x78 as in
+// fq_gemm_decode_kernel), the producer's pointers in place of the unfused-only ones.
+template <int MT, int PRO>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_pro_kernel(
+    const uint16_t *__restrict__ xh, int abits, const uint32_t *__restrict__ wpk, int Mall, int N, int K,
+    uint16_t *__restrict__ d, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC,
+    int xwin, int iq, int ir, const uint16_t *__restrict__ pin, const uint16_t *__restrict__ gamma,
+    uint16_t *__restrict__ res_out, float eps, int ldh) {
+    const DecodePro pro = {pin, gamma, res_out, eps, ldh};
+    decode_body<MT, 0, 0, true, false, 0, false, PRO, false>(nullptr, nullptr, xh, abits, wpk, Mall, N, K, d, nullptr,
+                                                             slabs, tickets, S, IPW, RC, xwin, iq, ir, 1, nullptr, pro);
+}
 
 // Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q
 // polls rank q's flag with system-scope loads, sleeping between polls), then acquire and advance
@@ -1562,18 +1575,20 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 #undef FQ_ABL
     }
 #endif
+    if constexpr (PRO != 0) {  // the fused producers (FUSE, S as planned, no debug output, no gather)
+        hipLaunchKernelGGL((fq_gemm_decode_pro_kernel<MT, PRO>), grid, block, lds, stream, a.xh, a.abits,
+                           (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, slabs, tickets, p.S, p.IPW, p.RC, p.xwin,
+                           p.NT * p.S / p.grid, p.NT * p.S % p.grid, a.pro.in, a.pro.gamma, a.pro.res_out, a.pro.eps,
+                           a.pro.ldh);
+        FQ_LAUNCH_CHECK();
+        return FQ_OK;
+    }
     if constexpr (!CH) {
-        if (PRO != 0 || a.gat) {  // the fused producers and the peer-store gather: the long argument list
-            if (a.gat)
-                hipLaunchKernelGGL((fq_gemm_decode_ext_kernel<MT, XS, SS, FUSE, DBG, 0, true>), grid, block, lds,
-                                   stream, a.xq, a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d,
-                                   a.acc_dbg, slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),
-                                   p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat, a.pro);
-            else
-                hipLaunchKernelGGL((fq_gemm_decode_ext_kernel<MT, XS, SS, FUSE, DBG, PRO, false>), grid, block, lds,
-                                   stream, a.xq, a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d,
-                                   a.acc_dbg, slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),
-                                   p.NT * p.S % (p.grid / p.NCH), p.NCH, nullptr, a.pro);
+        if (a.gat) {  // the peer-store gather: the long argument list
+            hipLaunchKernelGGL((fq_gemm_decode_ext_kernel<MT, XS, SS, FUSE, DBG, 0, true>), grid, block, lds, stream,
+                               a.xq, a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs,
+                               tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),
+                               p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat, a.pro);
             FQ_LAUNCH_CHECK();
             return FQ_OK;
         }
