@@ -613,8 +613,8 @@ __device__ __forceinline__ void decode_body(
 // The kernels around decode_body.  The plain one keeps the short argument list: its explicit
 // arguments and the hidden block count it reads stay within the first 128 bytes of the kernarg
 // segment -- 40 more bytes of (unused) arguments cost the plain launch ~2.5 % (A/B/A/B,
-// tools/ab_karg.sh) -- and only the peer-store gather takes the long one (the fused producers
-// have their own short list, fq_gemm_decode_pro_kernel).
+// tools/ab_karg.sh).  The peer-store gather and the fused producers have kernels of their own with
+// lists of the same length.
 #define FQ_DECODE_ARGS                                                                                              \
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,      \
         const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d,                          \
@@ -625,11 +625,16 @@ template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = fa
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(FQ_DECODE_ARGS) {
     decode_body<MT, XS, SS, FUSE, DBG, ABL, CH, 0, false>(FQ_DECODE_PASS, nullptr, DecodePro{});
 }
-template <int MT, int XS, int SS, bool FUSE, bool DBG, int PRO, bool GAT>
-__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ext_kernel(FQ_DECODE_ARGS,
-                                                                                   const fq_gather *__restrict__ gat,
-                                                                                   const DecodePro pro) {
-    decode_body<MT, XS, SS, FUSE, DBG, 0, false, PRO, GAT>(FQ_DECODE_PASS, gat, pro);
+// The peer-store gather's kernel: the same list with the gather descriptor in the debug output's
+// place (no debug output with a gather).
+template <int MT, int XS, int SS, bool FUSE>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_gather_kernel(
+    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
+    const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d,
+    const fq_gather *__restrict__ gat, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW,
+    int RC, int xwin, int iq, int ir, int NCH) {
+    decode_body<MT, XS, SS, FUSE, false, 0, false, 0, true>(xq, xs, xh, abits, wpk, Mall, N, K, d, nullptr, slabs,
+                                                            tickets, S, IPW, RC, xwin, iq, ir, NCH, gat, DecodePro{});
 }
 #undef FQ_DECODE_ARGS
 #undef FQ_DECODE_PASS
@@ -1583,16 +1588,17 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
-    if constexpr (!CH) {
-        if (a.gat) {  // the peer-store gather: the long argument list
-            hipLaunchKernelGGL((fq_gemm_decode_ext_kernel<MT, XS, SS, FUSE, DBG, 0, true>), grid, block, lds, stream,
-                               a.xq, a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs,
-                               tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),
-                               p.NT * p.S % (p.grid / p.NCH), p.NCH, a.gat, a.pro);
+    if constexpr (!CH && !DBG) {
+        if (a.gat) {  // the peer-store gather
+            hipLaunchKernelGGL((fq_gemm_decode_gather_kernel<MT, XS, SS, FUSE>), grid, block, lds, stream, a.xq, a.xs,
+                               a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.gat, slabs, tickets, p.S,
+                               p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH),
+                               p.NCH);
             FQ_LAUNCH_CHECK();
             return FQ_OK;
         }
     }
+    if (a.gat) return FQ_ERR_SHAPE;  // (no gather with the debug output or row chunks)
     hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH>), grid, block, lds, stream, a.xq, a.xs,
                        a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S,
                        p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH);
