@@ -5,7 +5,7 @@ R=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof gpurun_out/profiles
 P=gpurun_out/profiles  # merged back by gpurun; copy into profiles/ afterwards
-B="python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers"
+B="python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers --no-extra-configs"
 # 1. kernel trace + stats of the default bench (LLaMA-2-7B, M=1)
 echo "[profile_round] 1. kernel trace + stats of the default bench (LLaMA-2-7B, " ; date
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/kt -o run -- $B --steps 5 > gpurun_out/prof/kt.log 2>&1
