@@ -234,12 +234,13 @@ __device__ __forceinline__ void decode_body(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
     float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir,
-    int NCH, const fq_gather *__restrict__ gat, const DecodePro &pro) {
+    int NCH, const fq_gather *__restrict__ gat, const DecodePro &pro, int gridall = -1) {
+    if (gridall < 0) gridall = (int)gridDim.x;  // (the plain kernel passes it: no hidden-argument load)
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
     // second serial round trip before the first DMA; tools/stamps.py).
     asm volatile("" ::"s"(xq), "s"(xs), "s"(xh), "s"(abits), "s"(wpk), "s"(Mall), "s"(N), "s"(K), "s"(d), "s"(slabs),
-                 "s"(tickets), "s"(S), "s"(IPW), "s"(RC), "s"(xwin), "s"(iq), "s"(ir), "s"(gridDim.x));
+                 "s"(tickets), "s"(S), "s"(IPW), "s"(RC), "s"(xwin), "s"(iq), "s"(ir), "s"(gridall));
     if (CH) asm volatile("" ::"s"(NCH));
     using C = DecodeCfg<MT, XS, SS>;
     constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
@@ -259,7 +260,7 @@ __device__ __forceinline__ void decode_body(
     // math below costs the one-chunk kernel ~0.15 us per launch when it is not compiled out.
     const int c = CH ? (int)((unsigned)blockIdx.x % (unsigned)NCH) : 0;
     const int bid = CH ? (int)((unsigned)blockIdx.x / (unsigned)NCH) : (int)blockIdx.x;
-    const int grid = CH ? (int)(gridDim.x / (unsigned)NCH) : (int)gridDim.x;
+    const int grid = CH ? (int)((unsigned)gridall / (unsigned)NCH) : gridall;
     const int M = CH ? (Mall - MT * c < MT ? Mall - MT * c : MT) : Mall, ldx = Mall;
     if (CH) {
         xq += (size_t)MT * c * K;
@@ -621,9 +622,45 @@ __device__ __forceinline__ void decode_body(
         int32_t *__restrict__ acc_dbg, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW,    \
         int RC, int xwin, int iq, int ir, int NCH
 #define FQ_DECODE_PASS xq, xs, xh, abits, wpk, Mall, N, K, d, acc_dbg, slabs, tickets, S, IPW, RC, xwin, iq, ir, NCH
-template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false>
-__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(FQ_DECODE_ARGS) {
-    decode_body<MT, XS, SS, FUSE, DBG, ABL, CH, 0, false>(FQ_DECODE_PASS, nullptr, DecodePro{});
+// The plain kernel (the headline launch) takes 56 bytes of arguments -- five pointers and four
+// dwords of bit fields (decode_pack) -- which fq_gemm.hip's build preloads into SGPRs
+// (-amdgpu-kernarg-preload-count, Makefile): the launch reads no kernarg memory before its first
+// DMA (A/B x 3: 0.6-1 % per step, tools/ab_preload.sh).  The debug accumulator output takes the long
+// list (fq_gemm_decode_dbg_kernel).
+struct DecodePacked {
+    uint32_t w0, w1, w2, w3;
+};
+// w0 = N (21 bits) | abits << 21 (4) | xwin << 25 (6); w1 = G (13) | S << 13 (10) | NCH << 23 (4);
+// w2 = IPW (16) | RC << 16 (16); w3 = Mall (10) | ir << 10 (11) | grid << 21 (11)
+static bool decode_pack(int N, int K, int abits, int xwin, int S, int NCH, int IPW, int RC, int Mall, int ir,
+                        int grid, DecodePacked *p) {
+    const int G = K / FQ_GROUP;
+    if (N >= (1 << 21) || abits > 15 || xwin > 63 || G >= (1 << 13) || S >= (1 << 10) || NCH > 15 ||
+        IPW > 0xffff || RC > 0xffff || Mall >= (1 << 10) || ir >= (1 << 11) || grid >= (1 << 11))
+        return false;
+    p->w0 = (uint32_t)N | ((uint32_t)abits << 21) | ((uint32_t)xwin << 25);
+    p->w1 = (uint32_t)G | ((uint32_t)S << 13) | ((uint32_t)NCH << 23);
+    p->w2 = (uint32_t)IPW | ((uint32_t)RC << 16);
+    p->w3 = (uint32_t)Mall | ((uint32_t)ir << 10) | ((uint32_t)grid << 21);
+    return true;
+}
+template <int MT, int XS, int SS, bool FUSE, int ABL = 0, bool CH = false>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
+    const void *__restrict__ x, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk,
+    uint16_t *__restrict__ d, char *__restrict__ ws, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const int N = w0 & 0x1fffff, abits = (w0 >> 21) & 15, xwin = w0 >> 25;
+    const int K = (w1 & 0x1fff) * FQ_GROUP, S = (w1 >> 13) & 1023, NCH = w1 >> 23;
+    const int IPW = w2 & 0xffff, RC = w2 >> 16;
+    const int Mall = w3 & 1023, ir = (w3 >> 10) & 2047, grid = w3 >> 21;
+    const int iq = IPW - (ir != 0);  // items per WG: IPW = ceil, iq = floor (decode_plan)
+    decode_body<MT, XS, SS, FUSE, false, ABL, CH, 0, false>(
+        FUSE ? nullptr : reinterpret_cast<const int8_t *>(x), xs, FUSE ? reinterpret_cast<const uint16_t *>(x) : nullptr,
+        abits, wpk, Mall, N, K, d, nullptr, reinterpret_cast<float *>(ws + FQ_TICKET_BYTES),
+        reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, iq, ir, NCH, nullptr, DecodePro{}, grid);
+}
+template <int MT, int XS, int SS, bool FUSE, bool CH>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_dbg_kernel(FQ_DECODE_ARGS) {
+    decode_body<MT, XS, SS, FUSE, true, 0, CH, 0, false>(FQ_DECODE_PASS, nullptr, DecodePro{});
 }
 // The peer-store gather's kernel: the same list with the gather descriptor in the debug output's
 // place (no debug output with a gather).
@@ -1564,15 +1601,19 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
     float *slabs = p.S > 1 ? (float *)((char *)a.workspace + kTicketBytes) : nullptr;
     const size_t lds = decode_lds_bytes(p, a.M, a.N, a.K);
     const dim3 grid(p.grid), block(decode_waves(MT) * 64);
+    DecodePacked pk;
+    const int gw = p.grid / p.NCH, items = p.NT * p.S;
+    if (items / gw != p.IPW - (items % gw != 0) ||
+        !decode_pack(a.N, a.K, a.abits, p.xwin, p.S, p.NCH, p.IPW, p.RC, a.M, items % gw, p.grid, &pk))
+        return FQ_ERR_SHAPE;  // (never for the planner's decode plans; the packing's bounds)
+    const void *xarg = FUSE ? (const void *)a.xh : (const void *)a.xq;
 #ifdef FQ_DEV_ABLATION
     if (!DBG && !CH && MT == 4 && XS == 0 && SS == 0) {  // (the fused and the unfused kernel)
         const int abl = dev_ablation();
 #define FQ_ABL(v)                                                                                           \
     if (abl == v) {                                                                                           \
-        hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, v>), grid, block, lds, stream, a.xq,  \
-                           a.xs, a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg,        \
-                           slabs, tickets, p.S, p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH),              \
-                           p.NT * p.S % (p.grid / p.NCH), p.NCH);                                               \
+        hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, v>), grid, block, lds, stream, xarg, a.xs, \
+                           (const uint32_t *)a.wpk, a.d, (char *)a.workspace, pk.w0, pk.w1, pk.w2, pk.w3);      \
         FQ_LAUNCH_CHECK();                                                                                    \
         return FQ_OK;                                                                                         \
     }
@@ -1599,9 +1640,14 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         }
     }
     if (a.gat) return FQ_ERR_SHAPE;  // (no gather with the debug output or row chunks)
-    hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, DBG, 0, CH>), grid, block, lds, stream, a.xq, a.xs,
-                       a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S,
-                       p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH);
+    if constexpr (DBG) {
+        hipLaunchKernelGGL((fq_gemm_decode_dbg_kernel<MT, XS, SS, FUSE, CH>), grid, block, lds, stream, a.xq, a.xs,
+                           a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.acc_dbg, slabs, tickets, p.S,
+                           p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH), p.NCH);
+    } else {
+        hipLaunchKernelGGL((fq_gemm_decode_kernel<MT, XS, SS, FUSE, 0, CH>), grid, block, lds, stream, xarg, a.xs,
+                           (const uint32_t *)a.wpk, a.d, (char *)a.workspace, pk.w0, pk.w1, pk.w2, pk.w3);
+    }
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
