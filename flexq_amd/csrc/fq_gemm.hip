@@ -239,8 +239,14 @@ __device__ __forceinline__ void decode_body(
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
     // second serial round trip before the first DMA; tools/stamps.py).
-    asm volatile("" ::"s"(xq), "s"(xs), "s"(xh), "s"(abits), "s"(wpk), "s"(Mall), "s"(N), "s"(K), "s"(d), "s"(slabs),
-                 "s"(tickets), "s"(S), "s"(IPW), "s"(RC), "s"(xwin), "s"(iq), "s"(ir), "s"(gridall));
+    // (The fused producers' kernel passes the output, workspace and residual output after its
+    // preloaded arguments: they are needed only after the first window, so they stay out of this batch.)
+    if (PRO == 0)
+        asm volatile("" ::"s"(xq), "s"(xs), "s"(xh), "s"(abits), "s"(wpk), "s"(Mall), "s"(N), "s"(K), "s"(d),
+                     "s"(slabs), "s"(tickets), "s"(S), "s"(IPW), "s"(RC), "s"(xwin), "s"(iq), "s"(ir), "s"(gridall));
+    else
+        asm volatile("" ::"s"(xh), "s"(abits), "s"(wpk), "s"(Mall), "s"(N), "s"(K), "s"(S), "s"(IPW), "s"(RC),
+                     "s"(xwin), "s"(iq), "s"(ir), "s"(gridall), "s"(pro.in), "s"(pro.gamma), "s"(pro.ldh));
     if (CH) asm volatile("" ::"s"(NCH));
     using C = DecodeCfg<MT, XS, SS>;
     constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
@@ -675,17 +681,22 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_gather_k
 }
 #undef FQ_DECODE_ARGS
 #undef FQ_DECODE_PASS
-// The fused producers' kernel: the plain argument list's length (hidden arguments at 0x78 as in
-// fq_gemm_decode_kernel), the producer's pointers in place of the unfused-only ones.
+// The fused producers' kernel: what the first DMA needs -- the window sources and the packed
+// fields -- in the 56 preloaded bytes, the output, workspace and residual output after them (loaded
+// at entry, first waited on after the window has arrived).
 template <int MT, int PRO>
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_pro_kernel(
-    const uint16_t *__restrict__ xh, int abits, const uint32_t *__restrict__ wpk, int Mall, int N, int K,
-    uint16_t *__restrict__ d, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC,
-    int xwin, int iq, int ir, const uint16_t *__restrict__ pin, const uint16_t *__restrict__ gamma,
-    uint16_t *__restrict__ res_out, float eps, int ldh) {
+    const uint16_t *__restrict__ xh, const uint32_t *__restrict__ wpk, const uint16_t *__restrict__ pin,
+    const uint16_t *__restrict__ gamma, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int ldh, float eps,
+    uint16_t *__restrict__ d, char *__restrict__ ws, uint16_t *__restrict__ res_out) {
+    const int N = w0 & 0x1fffff, abits = (w0 >> 21) & 15, xwin = w0 >> 25;
+    const int K = (w1 & 0x1fff) * FQ_GROUP, S = (w1 >> 13) & 1023;
+    const int IPW = w2 & 0xffff, RC = w2 >> 16;
+    const int Mall = w3 & 1023, ir = (w3 >> 10) & 2047, grid = w3 >> 21;
     const DecodePro pro = {pin, gamma, res_out, eps, ldh};
-    decode_body<MT, 0, 0, true, false, 0, false, PRO, false>(nullptr, nullptr, xh, abits, wpk, Mall, N, K, d, nullptr,
-                                                             slabs, tickets, S, IPW, RC, xwin, iq, ir, 1, nullptr, pro);
+    decode_body<MT, 0, 0, true, false, 0, false, PRO, false>(
+        nullptr, nullptr, xh, abits, wpk, Mall, N, K, d, nullptr, reinterpret_cast<float *>(ws + FQ_TICKET_BYTES),
+        reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, IPW - (ir != 0), ir, 1, nullptr, pro, grid);
 }
 
 // Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q
@@ -1622,10 +1633,10 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
     }
 #endif
     if constexpr (PRO != 0) {  // the fused producers (FUSE, S as planned, no debug output, no gather)
-        hipLaunchKernelGGL((fq_gemm_decode_pro_kernel<MT, PRO>), grid, block, lds, stream, a.xh, a.abits,
-                           (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, slabs, tickets, p.S, p.IPW, p.RC, p.xwin,
-                           p.NT * p.S / p.grid, p.NT * p.S % p.grid, a.pro.in, a.pro.gamma, a.pro.res_out, a.pro.eps,
-                           a.pro.ldh);
+        if (p.NCH != 1) return FQ_ERR_SHAPE;  // (the producer plans have one row chunk)
+        hipLaunchKernelGGL((fq_gemm_decode_pro_kernel<MT, PRO>), grid, block, lds, stream, a.xh,
+                           (const uint32_t *)a.wpk, a.pro.in, a.pro.gamma, pk.w0, pk.w1, pk.w2, pk.w3, a.pro.ldh,
+                           a.pro.eps, a.d, (char *)a.workspace, a.pro.res_out);
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
