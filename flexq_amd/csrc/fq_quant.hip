@@ -18,17 +18,19 @@
 // =============================================================================================
 // IDX: index type -- 32-bit when M*K fits (64-bit division alone costs ~100 instructions per
 // lane, comparable to the quantizer itself), 64-bit otherwise.
+// The arguments (at most 56 bytes, the wave count passed explicitly: no hidden-argument read) are
+// preloaded into SGPRs (Makefile KPRELOAD): the batch-16 step runs one such launch per linear.
 template <int MODE, typename IDX>
 __global__ __launch_bounds__(256) void fq_quantize_act_kernel(
-    const uint16_t *__restrict__ x, int M, int K, int bits, int8_t *__restrict__ xq,
+    const uint16_t *__restrict__ x, int M, int K, int bits, int nwaves_, int8_t *__restrict__ xq,
     uint16_t *__restrict__ xs, int32_t *__restrict__ planes, uint16_t *__restrict__ xs_dup) {
     using U = typename std::conditional<sizeof(IDX) == 4, unsigned, unsigned long>::type;
     const int G = K / FQ_GROUP;
     const IDX T = (IDX)M * G;  // total groups
     const int lane = threadIdx.x & 63;
     const int sub = lane & 15;  // position inside the group
-    const IDX wave = (IDX)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const IDX nwaves = (IDX)((gridDim.x * blockDim.x) >> 6);
+    const IDX wave = (IDX)((blockIdx.x * 256u + threadIdx.x) >> 6);
+    const IDX nwaves = (IDX)nwaves_;
 
     for (IDX chunk = wave; chunk * 4 < T; chunk += nwaves) {
         const IDX gi = chunk * 4 + (lane >> 4);  // flat group index of this lane
@@ -83,12 +85,13 @@ extern "C" fq_status fq_quantize_act(const uint16_t *x, int M, int K, int abits,
     if (M <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     const long groups = (long)M * (K / FQ_GROUP);
+    const int grid = quant_grid(groups);
     if (groups * FQ_GROUP < (1L << 31))
-        hipLaunchKernelGGL((fq_quantize_act_kernel<0, int>), dim3(quant_grid(groups)), dim3(256), 0,
-                           (hipStream_t)stream, x, M, K, abits, xq, xs, nullptr, nullptr);
+        hipLaunchKernelGGL((fq_quantize_act_kernel<0, int>), dim3(grid), dim3(256), 0, (hipStream_t)stream, x, M, K,
+                           abits, grid * 4, xq, xs, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((fq_quantize_act_kernel<0, long>), dim3(quant_grid(groups)), dim3(256), 0,
-                           (hipStream_t)stream, x, M, K, abits, xq, xs, nullptr, nullptr);
+        hipLaunchKernelGGL((fq_quantize_act_kernel<0, long>), dim3(grid), dim3(256), 0, (hipStream_t)stream, x, M, K,
+                           abits, grid * 4, xq, xs, nullptr, nullptr);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
@@ -100,8 +103,9 @@ extern "C" fq_status fq_ref_quantize_bit_packing(const uint16_t *x, int32_t *pac
     if (M <= 0 || K <= 0 || K % FQ_GROUP || (M > 8 && M % 8)) return FQ_ERR_SHAPE;
     if (bits != 6 && bits != 8) return FQ_ERR_BITS;
     const long groups = (long)M * (K / FQ_GROUP);
-    hipLaunchKernelGGL((fq_quantize_act_kernel<1, long>), dim3(quant_grid(groups)), dim3(256), 0,
-                       (hipStream_t)stream, x, M, K, bits, nullptr, nullptr, packed, x_scale_dup);
+    const int grid = quant_grid(groups);
+    hipLaunchKernelGGL((fq_quantize_act_kernel<1, long>), dim3(grid), dim3(256), 0, (hipStream_t)stream, x, M, K, bits,
+                       grid * 4, nullptr, nullptr, packed, x_scale_dup);
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
