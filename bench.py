@@ -12,14 +12,16 @@ input, so by default they run as one linear over the concatenated weight image [
 launch), the whole step captured into one HIP graph.
 
 Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself through a child torchrun
-when it is not already under one): by default every linear is column-parallel over the N GPUs
-(BASELINE config C4's scheme): each rank packs and streams only its N/P rows,
-then ONE RCCL all-gather per linear assembles the dequantized fp16 output over xGMI; total work
-is fixed ("scaling": "strong"), `value` is the whole model's TFLOPS-equiv per step time (max
-over ranks).  The same line reports the step without the gathers (GEMM only), the per-rank HBM
-fraction, the gather bytes, the same model as independent replicas (`replicas`, --parallel dp:
-no data-path collective, weak scaling) and the LLaMA-2-70B column-parallel stack
-(`c4_llama2_70b_tp`).
+when it is not already under one): by default (`--parallel dp`) every GPU runs the whole stack on
+its own token stream -- decoding sequences are independent units, so they are partitioned over
+the ranks with no data-path collective ("scaling": "weak", `value` = all ranks' tokens per the
+max-over-ranks step time).  The north-star split of the same stack is measured beside it in the
+same line (`tp`: every linear column-parallel over the N GPUs, SURVEY.md §8(e), each rank packs
+and streams only its N/P rows, ONE RCCL all-gather per linear assembles the dequantized fp16
+output over xGMI; total work fixed, strong scaling; `tp_peer_gather`: the all-gather fused into
+the GEMM epilogue), as is BASELINE config C4, the LLaMA-2-70B column-parallel stack
+(`c4_llama2_70b_tp`).  `--parallel tp` makes the column-parallel step the `value` (then
+`replicas` is the section beside it).
 
 Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
 linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
@@ -687,11 +689,13 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
-    ap.add_argument("--parallel", choices=["dp", "tp"], default=None,
-                    help="N > 1: tp (default) = every linear column-sharded over the N GPUs + one RCCL "
-                         "all-gather per linear, total work fixed (strong scaling, SURVEY.md §8(e)); "
-                         "dp = independent replicas, one token stream per GPU (weak scaling)")
+    ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
+                    help="N > 1, what `value` measures: dp (default) = independent replicas, one token stream "
+                         "per GPU, no data-path collective (weak scaling); tp = every linear column-sharded over "
+                         "the N GPUs + one all-gather per linear, total work fixed (strong scaling, SURVEY.md "
+                         "§8(e)).  The other one is measured beside it in the same line (`tp` / `replicas`)")
     ap.add_argument("--no-replicas", action="store_true", help="N > 1, tp: skip the replica (dp) measurement")
+    ap.add_argument("--no-tp", action="store_true", help="N > 1, dp: skip the column-parallel (tp) measurement")
     ap.add_argument("--no-peer", action="store_true",
                     help="N > 1, tp: skip the peer-store gather variant (all-gather fused into the GEMM epilogue)")
     ap.add_argument("--no-c4", action="store_true",
@@ -727,8 +731,7 @@ def main():
     layers, M, lins, desc = cfg
     merge = not a.no_merge
     launch_lins = launch_list(lins, merge)
-    parallel = a.parallel or ("tp" if world > 1 else "dp")
-    tp = world if parallel == "tp" else 1  # ranks one linear is sharded over
+    tp = world if a.parallel == "tp" else 1  # ranks one linear is sharded over
     prefill = M > PREFILL_M
     n_lin = layers * len(launch_lins)
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
@@ -863,9 +866,22 @@ def main():
             "method": "graph of the step's prefill GEMM launches on pre-quantized codes (the quantize "
                       "launches excluded), HIP events on the capture stream; TOPS = 2*M*N*K / launch time",
         }
+    def tp_summary(rr):
+        return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in rr.items()
+                if k not in ("elapsed", "flops_step", "finite", "final")}
+    if world > 1 and tp == 1 and not a.no_tp:
+        # the north-star split of the same stack, measured beside the replicas: every
+        # linear column-parallel over the N GPUs + one RCCL all-gather per linear (strong scaling)
+        def tp_rccl():
+            rr = measure_tp(ctx, cfg, merge, world, a.steps, a.warmup)
+            return {"what": f"tp{world}: the same stack, every linear column-parallel (N/{world} rows per rank) "
+                            "+ one RCCL all_gather_into_tensor of its fp16 output per linear (strong scaling)",
+                    "value": round(rr["flops_step"] * a.steps / rr["elapsed"] / 1e12, 4), "unit": "TFLOPS-equiv",
+                    "tok_per_s": round(M * a.steps / rr["elapsed"], 2), **tp_summary(rr),
+                    "finite": rr["finite"], "hbm_frac_per_rank": round(rr["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
+        optional(res, "tp", tp_rccl, ctx)
     if tp > 1:
-        res["tp"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()
-                     if k not in ("elapsed", "flops_step", "finite", "final")}
+        res["tp"] = tp_summary(r)
         res["tp"]["gather"] = gather_impl
         res["tp"]["rccl_ms_per_step"] = round(r_rccl["ms_per_step"], 4)
         res["tp"]["hbm_frac_per_rank"] = round(r["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)
@@ -883,9 +899,10 @@ def main():
                         "ms_per_step": round(el_dp / a.steps * 1e3, 4)}
             need = cfg[0] * sum(ops.packed_w_bytes(N, K) for (_, N, K, _) in launch_lins)
             optional(res, "replicas", replicas, ctx, need_bytes=need)
+    if world > 1:
         if not a.no_peer and M <= 32:  # the all-gather fused into the GEMM epilogue
             def tp_peer(c):
-                rp = measure_tp(ctx, c, merge, tp, max(2, a.steps // 2), max(1, a.warmup // 2), peer=True)
+                rp = measure_tp(ctx, c, merge, world, max(2, a.steps // 2), max(1, a.warmup // 2), peer=True)
                 return {"what": "the same column-parallel stack, each all-gather fused into its GEMM's epilogue: "
                                 "peer stores into IPC-mapped gather buffers + one wait launch per linear "
                                 "(fq_linear_w6ax_gather / fq_gather_wait) instead of an RCCL all_gather",
@@ -894,7 +911,9 @@ def main():
                         "ms_per_step": round(rp["ms_per_step"], 4),
                         "gemm_only_ms_per_step": round(rp["gemm_only_ms_per_step"], 4),
                         "finite": rp["finite"], "graph": rp["graph"]}
-            rp = peer_sec.get("p")
+            rp = peer_sec.get("p") if tp > 1 else None
+            if tp == 1 and not a.no_tp:
+                optional(res, "tp_peer_gather", lambda: tp_peer(cfg), ctx)
             if rp is not None and "final" in rp:
                 res["tp_peer_gather"] = {
                     "what": "the same column-parallel stack, each all-gather fused into its GEMM's epilogue: peer "
