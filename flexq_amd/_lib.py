@@ -57,6 +57,8 @@ _SIGS = {
     "fq_ref_quantize_bit_packing": ([P, P, P, I, I, I, P], I),
     "fq_import_ref_w": ([P, P, I, I, P, P], I),
     "fq_import_ref_x": ([P, P, I, I, I, P, P, P], I),
+    "fq_planes_act_scratch_bytes": ([I, I, I], SZ),
+    "fq_gemm_w6ax_planes": ([P, P, P, I, I, I, I, P, P, P, P, SZ, P], I),
     "fq_bmma_scratch_bytes": ([I, I, I], SZ),
     "fq_bmma_image_scratch_bytes": ([I, I, I], SZ),
     "fq_rmsnorm_quantize": ([P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),

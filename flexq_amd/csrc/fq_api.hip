@@ -191,7 +191,8 @@ extern "C" fq_status fq_bmma_exec(fq_bmma_state *st, fq_stream_t stream) {
             return s;
         st->prepared = 1;
     }
-    if ((s = fq_import_ref_x(st->X, st->X_SCALE, st->M, st->K, st->x_bits, xq, xs, stream)) != FQ_OK) return s;
-    return fq_gemm_w6ax(xq, xs, st->w_format == FQ_W_BITPLANES ? img : st->W, st->M, st->N, st->K, st->x_bits,
-                        st->D, nullptr, ws, fq_gemm_workspace_bytes(st->M, st->N, st->K), stream);
+    // decode sizes: one launch, the planes unpacked inside the GEMM; otherwise imported into xq / xs
+    return fq_gemm_w6ax_planes(st->X, st->X_SCALE, st->w_format == FQ_W_BITPLANES ? img : st->W, st->M, st->N,
+                               st->K, st->x_bits, st->D, xq, xs, ws, fq_gemm_workspace_bytes(st->M, st->N, st->K),
+                               stream);
 }

@@ -156,11 +156,8 @@ void exec_impl(FQBMMAOpState &st, hipStream_t s) {
     const size_t wsr = ws_region(a.M, a.N, a.K);
     int8_t *xq = reinterpret_cast<int8_t *>(base + wsr);
     uint16_t *xs = reinterpret_cast<uint16_t *>(base + wsr + align256((size_t)a.M * a.K));
-    if (!report(fq_import_ref_x(a.X, reinterpret_cast<const uint16_t *>(a.X_SCALE), a.M, a.K, XB, xq, xs, (fq_stream_t)s),
-                "FQBMMA exec: activation import"))
-        return;
-    report(fq_gemm_w6ax(xq, xs, img, a.M, a.N, a.K, XB, reinterpret_cast<uint16_t *>(a.D), nullptr, base, wsr,
-                        (fq_stream_t)s),
+    report(fq_gemm_w6ax_planes(a.X, reinterpret_cast<const uint16_t *>(a.X_SCALE), img, a.M, a.N, a.K, XB,
+                               reinterpret_cast<uint16_t *>(a.D), xq, xs, base, wsr, (fq_stream_t)s),
            "FQBMMA exec");
 }
 

@@ -308,6 +308,32 @@ __device__ __forceinline__ void decode_body(
     const int xwb = FUSE ? decode_xwin_bytes(ngmax, M, xwin) : 0;   // (PRO: the next windows)
     const long ldh = PRO ? (long)pro.ldh : (long)K;
     auto x_fetch = [&](int r0) {  // pairs [r0, r0 + xwin) -> xh_st
+        if (PRO == 3) {
+            // Reference bit planes (int32 [K/128][M/c][b][c][4], c = min(M, 8), k0 at bit 31;
+            // engine/src/pack/bit_packing.cu:104-131): a pair's plane p is 16 contiguous bytes.
+            // 8 lanes per pair (lane & 7 = plane, planes >= b re-read plane b - 1), 8 pairs per
+            // instruction, window slot = 128 B per pair.
+            const int ch = M < 8 ? M : 8, q = (lane & 7) < abits ? (lane & 7) : abits - 1;
+            const int32_t *planes = reinterpret_cast<const int32_t *>(xh);
+            for (int c = 0; c < xwin && r0 + c < R; c += 8) {
+                int rg = r0 + c + (lane >> 3);
+                rg = rg < R ? rg : R - 1;
+                const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+                const long wd = (long)(ga + j) * (M * abits * 4) + (row / ch) * (abits * ch * 4) + q * (ch * 4) + (row % ch) * 4;
+                __builtin_amdgcn_global_load_lds(planes + wd, LDS_PTR(xh_st + c * 128), 16, 0, 0);
+            }
+            if (r0 == 0) {  // x-scales: the reference's duplicated pairs (half[K/128][2 ceil4(M)],
+                            // SCALE_PACKING_A) are one dword per (group, row) -> xs_st slots
+                const int ld2 = (M + 3) / 4 * 4;
+                const uint32_t *xsd = reinterpret_cast<const uint32_t *>(pro.in);
+                for (int i0 = 0; i0 < ng; i0 += 64 / XSR) {
+                    const int i = i0 + lane / XSR, row = lane % XSR;
+                    __builtin_amdgcn_global_load_lds(xsd + (long)(ga + (i < ng ? i : ng - 1)) * ld2 + (row < M ? row : M - 1),
+                                                     LDS_PTR(xs_st + i0 * XSR * 4), 4, 0, 0);
+                }
+            }
+            return;
+        }
         for (int c = 0; c < xwin && r0 + c < R; c += 4) {
             int rg = r0 + c + (lane >> 4);
             rg = rg < R ? rg : R - 1;
@@ -357,6 +383,35 @@ __device__ __forceinline__ void decode_body(
                 uint2 codes1;
                 const uint16_t sh1 = quant_group16(v1, abits, codes1);
                 x_store(rg + 4, codes1, sh1);
+            }
+        }
+    };
+    // PRO 3: bit planes -> int8 codes.  Lane 8 pp + q builds the 16 codes of chunk q (k = 16 q ..
+    // 16 q + 15) of pair pp: per plane, bit-reverse the word (value k0 + i at bit i), then spread
+    // each nibble over four bytes (x * 0x00204081 & 0x01010101) and add it in with weight 2^p, the
+    // top plane with 256 - 2^(b-1) (the sign bit of a b-bit two's complement value, sign-extended
+    // to the int8 byte).  The bytes never carry into each other (sum <= 255).
+    auto x_unpack = [&](int r0) {
+        const uint32_t sgn = 256u - (1u << (abits - 1));
+        for (int c = 0; c < xwin && r0 + c < R; c += 8) {
+            const int pp = c + (lane >> 3), rg = r0 + pp, q = lane & 7;
+            const uint32_t pa = lds_addr(xh_st + pp * 128 + (q >> 1) * 4);
+            uint32_t w[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) w[p] = ds_read_b32(pa + p * 16);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]),
+                         "+v"(w[5]), "+v"(w[6]), "+v"(w[7])::"memory");
+            uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+                const uint32_t mul = p < abits - 1 ? (1u << p) : (p == abits - 1 ? sgn : 0u);
+                const uint32_t h = __builtin_bitreverse32(w[p]) >> (16 * (q & 1));
+#pragma unroll
+                for (int dd = 0; dd < 4; dd++) o[dd] += ((((h >> (4 * dd)) & 15u) * 0x00204081u) & 0x01010101u) * mul;
+            }
+            if (pp < xwin && rg < R) {
+                const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+                ds_write_b128(lds_addr(x_st + rg * 128 + xswz(row, q)), v4i{(int)o[0], (int)o[1], (int)o[2], (int)o[3]});
             }
         }
     };
@@ -462,6 +517,8 @@ __device__ __forceinline__ void decode_body(
             const uint16_t sh = quant_group16(rms_apply8(r, make_uint4(gg[0], gg[1], gg[2], gg[3]), rms_scale(ss, K, pro.eps)),
                                               abits, codes);
             x_store(lane >> 4, codes, sh);
+        } else if (PRO == 3) {
+            x_unpack(0);
         } else {
             x_quant(0);
         }
@@ -474,7 +531,10 @@ __device__ __forceinline__ void decode_body(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous window was read
             x_fetch(r0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            x_quant(r0);
+            if (PRO == 3)
+                x_unpack(r0);
+            else
+                x_quant(r0);
         }
     }
 
@@ -755,9 +815,6 @@ constexpr int PF_VM_A = 5, PF_VM_W = 3;            // per wave and group: A + sc
 // s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
 constexpr int vmcnt_only(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
-__device__ __forceinline__ void ds_write_b128(uint32_t a, v4i v) {
-    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
 template <int OFF>
 __device__ __forceinline__ uint32_t ds_read_b32_at(uint32_t a) {
     uint32_t v;
@@ -1754,6 +1811,44 @@ fq_status fq_decode_linear_pro(int pro, const uint16_t *xh, const DecodePro &pro
         case 16: return launch_decode<16, 0, 0, true, false, false, 2>(p, a, s);
         default: return launch_decode<32, 0, 0, true, false, false, 2>(p, a, s);
     }
+}
+
+// The reference's bit-plane activations (FQBMMAExecFn_t's X + duplicated X_SCALE, the wrapper's
+// gemm(const int* A ...)) unpacked inside the decode GEMM's prologue (PRO 3): one launch wherever
+// fq_linear_w6ax would fuse its quantizer; otherwise fq_import_ref_x into the caller's buffers,
+// then fq_gemm_w6ax.  Bit-identical either way (the same plan, S and reduction order).
+static bool planes_fuse(int M, int N, int K, DecodePlan *p) { return (M <= 8 || M % 8 == 0) && decode_fuse(M, N, K, p, 3); }
+extern "C" size_t fq_planes_act_scratch_bytes(int M, int N, int K) {
+    DecodePlan p;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || planes_fuse(M, N, K, &p)) return 0;
+    return (size_t)M * K + (size_t)M * (K / FQ_GROUP) * 2;
+}
+extern "C" fq_status fq_gemm_w6ax_planes(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, const void *w_packed,
+                                         int M, int N, int K, int abits, uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf,
+                                         void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+    if (!x_bitplanes || !x_scale_dup || !w_packed || !d) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || (M > 8 && M % 8)) return FQ_ERR_SHAPE;
+    if ((size_t)((N + 15) / 16) > kTicketBytes / 4) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    DecodePlan p;
+    if (planes_fuse(M, N, K, &p)) {
+        const size_t need = fq_gemm_workspace_bytes(M, N, K);
+        if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
+        const DecodePro pro = {x_scale_dup, nullptr, nullptr, 0.f, K};
+        DecodeArgs a = {nullptr, nullptr, reinterpret_cast<const uint16_t *>(x_bitplanes), abits, w_packed, M, N, K,
+                        d, nullptr, workspace, nullptr, pro};
+        hipStream_t s = (hipStream_t)stream;
+        switch (p.MT) {
+            case 4: return launch_decode<4, 0, 0, true, false, false, 3>(p, a, s);
+            case 8: return launch_decode<8, 0, 0, true, false, false, 3>(p, a, s);
+            case 16: return launch_decode<16, 0, 0, true, false, false, 3>(p, a, s);
+            default: return launch_decode<32, 0, 0, true, false, false, 3>(p, a, s);
+        }
+    }
+    if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
+    const fq_status st = fq_import_ref_x(x_bitplanes, x_scale_dup, M, K, abits, xq_buf, xs_buf, stream);
+    if (st != FQ_OK) return st;
+    return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace, workspace_bytes, stream);
 }
 
 fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,

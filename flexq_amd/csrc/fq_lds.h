@@ -23,6 +23,14 @@ __device__ __forceinline__ v2u ds_read_b64(uint32_t a) {
 __device__ __forceinline__ void ds_write_b64(uint32_t a, uint2 v) {
     asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+__device__ __forceinline__ void ds_write_b128(uint32_t a, v4i v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t ds_read_b32(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
 __device__ __forceinline__ void ds_write_b32(uint32_t a, uint32_t v) {
     asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }

@@ -380,6 +380,37 @@ def import_ref_w(planes, ws, N, K):
     return out
 
 
+def gemm_w6ax_planes(planes, dup, wpk, M, N, K, bits, out=None):
+    """GEMM straight from the reference's bit-plane activations + duplicated x-scales (the X /
+    X_SCALE of FQBMMAExecFn_t, FLEXQGEMMWrapper::gemm(const int* A ...)): one launch at decode
+    sizes (the planes unpacked in the GEMM prologue), import + GEMM otherwise."""
+    _dev(planes, torch.int32, "planes", 1)
+    _dev(dup, torch.float16, "x_scale_dup", 2)
+    _k_ok(K)
+    _rows_ok(M)
+    _need(bits in (6, 8), "bits must be 6 or 8")
+    _need(planes.numel() == bits * M * (K // 32), "planes size does not match [M,K]")
+    _need(tuple(dup.shape) == (K // GROUP, 2 * ((M + 3) // 4 * 4)), "x_scale_dup must be [K/128, 2*ceil4(M)]")
+    _img_ok(wpk, N, K)
+    dev = planes.device
+    for t in (dup, wpk):
+        _need(t.device == dev, "all operands must be on one device")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=dev)
+    else:
+        _dev(out, torch.float16, "out", 2)
+        _need(tuple(out.shape) == (M, N), "out shape mismatch")
+    xq = xs = None
+    if int(_lib.load().fq_planes_act_scratch_bytes(M, N, K)):
+        xq = torch.empty((M, K), dtype=torch.int8, device=dev)
+        xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=dev)
+    s = _stream(planes)
+    wbuf = workspace(dev, gemm_workspace_bytes(M, N, K), s.value)
+    _lib.call("fq_gemm_w6ax_planes", _ptr(planes), _ptr(dup), _ptr(wpk), M, N, K, bits, _ptr(out), _ptr(xq),
+              _ptr(xs), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return out
+
+
 def import_ref_x(planes, dup, M, K, bits):
     _dev(planes, torch.int32, "planes", 1)
     _dev(dup, torch.float16, "x_scale_dup", 2)

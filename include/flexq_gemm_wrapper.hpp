@@ -85,12 +85,11 @@ class FLEXQGEMMWrapper {
         if (!img) return;
         Scratch sc;
         if (!scratch(M, N, K, stream, &sc)) return;
-        if (!report(fq_import_ref_x(A, reinterpret_cast<const uint16_t *>(x_scale), M, K, x_bits_, sc.xq, sc.xs,
-                                    (fq_stream_t)stream),
-                    "gemm: activation import"))
-            return;
-        report(fq_gemm_w6ax(sc.xq, sc.xs, img, M, N, K, x_bits_, reinterpret_cast<uint16_t *>(D), nullptr, sc.ws,
-                            sc.ws_bytes, (fq_stream_t)stream),
+        // decode sizes: the planes are unpacked inside the GEMM (one launch); otherwise imported
+        // into the wrapper's scratch first
+        report(fq_gemm_w6ax_planes(A, reinterpret_cast<const uint16_t *>(x_scale), img, M, N, K, x_bits_,
+                                   reinterpret_cast<uint16_t *>(D), sc.xq, sc.xs, sc.ws, sc.ws_bytes,
+                                   (fq_stream_t)stream),
                "gemm");
     }
 

@@ -222,6 +222,19 @@ fq_status fq_import_ref_w(const int32_t *w_bitplanes, const uint16_t *w_scale, i
 /* Reference bit-plane activations + duplicated scales -> xq int8 [M][K] + xs [K/128][M]. */
 fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, int M, int K,
                           int bits, int8_t *xq, uint16_t *xs, fq_stream_t stream);
+/* GEMM straight from the reference's bit-plane activations: the X / X_SCALE operands of
+ * FQBMMAExecFn_t (flexq_bmma_op.h:187-188) and of FLEXQGEMMWrapper::gemm(const int* A ...)
+ * (flexq_gemm_wrapper.cu:21-97; FT's decoder attention calls it with the packed output of its
+ * fused RMSNorm, LlamaV2DecoderSelfAttentionLayer.cc:653).  Where fq_linear_w6ax would fuse its
+ * quantizer (decode sizes) the planes are unpacked inside the GEMM's prologue: ONE launch, no
+ * scratch.  Otherwise fq_import_ref_x writes xq_buf / xs_buf (fq_planes_act_scratch_bytes: M*K
+ * bytes of codes + 2*M*(K/128) of scales, 0 when fused) and fq_gemm_w6ax follows.  Output
+ * bit-identical to fq_import_ref_x + fq_gemm_w6ax.  M <= 8 or M % 8 == 0 (the plane layout);
+ * workspace as for fq_gemm_w6ax. */
+size_t fq_planes_act_scratch_bytes(int M, int N, int K);
+fq_status fq_gemm_w6ax_planes(const int32_t *x_bitplanes, const uint16_t *x_scale_dup, const void *w_packed,
+                              int M, int N, int K, int bits, uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf,
+                              void *workspace, size_t workspace_bytes, fq_stream_t stream);
 
 /* FQBMMAOpState-style two-call interface (flexq_bmma_op.h:19-34, FQBMMAInitFn_t / FQBMMAExecFn_t
  * at :187-188): init validates and records the arguments -- no launch, and no device-attribute
