@@ -1522,7 +1522,9 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused, int pro = 0) {
     }
 #endif
     const int ngw = ((G + p.S - 1) / p.S + NW - 1) / NW;
-    p.cost4 = (int)best + (fused ? ngw * M : kSplitQuantCost4);
+    // (pro 3, bit planes: the unpack costs about half the quantizer per pair -- M = 2..16 A/B of the
+    // forced-fuse variant against import + GEMM)
+    p.cost4 = (int)best + (fused ? (pro == 3 ? (ngw * M + 1) / 2 : ngw * M) : kSplitQuantCost4);
     const int items = NT * p.S;
     p.grid = items < cus ? items : cus;
     p.IPW = (items + p.grid - 1) / p.grid;
@@ -1817,7 +1819,18 @@ fq_status fq_decode_linear_pro(int pro, const uint16_t *xh, const DecodePro &pro
 // gemm(const int* A ...)) unpacked inside the decode GEMM's prologue (PRO 3): one launch wherever
 // fq_linear_w6ax would fuse its quantizer; otherwise fq_import_ref_x into the caller's buffers,
 // then fq_gemm_w6ax.  Bit-identical either way (the same plan, S and reduction order).
-static bool planes_fuse(int M, int N, int K, DecodePlan *p) { return (M <= 8 || M % 8 == 0) && decode_fuse(M, N, K, p, 3); }
+#ifndef FQ_PLANES_FORCE_FUSE
+#define FQ_PLANES_FORCE_FUSE 0  // (development: 1 = unpack in the prologue whenever it fits, A/B tooling)
+#endif
+static bool planes_fuse(int M, int N, int K, DecodePlan *p) {
+    if (!(M <= 8 || M % 8 == 0)) return false;
+    if (FQ_PLANES_FORCE_FUSE) {
+        if (M > 32) return false;
+        *p = decode_plan(M, N, K, true, 3);
+        return p->fits;
+    }
+    return decode_fuse(M, N, K, p, 3);
+}
 extern "C" size_t fq_planes_act_scratch_bytes(int M, int N, int K) {
     DecodePlan p;
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || planes_fuse(M, N, K, &p)) return 0;

@@ -225,8 +225,8 @@ fq_status fq_import_ref_x(const int32_t *x_bitplanes, const uint16_t *x_scale_du
 /* GEMM straight from the reference's bit-plane activations: the X / X_SCALE operands of
  * FQBMMAExecFn_t (flexq_bmma_op.h:187-188) and of FLEXQGEMMWrapper::gemm(const int* A ...)
  * (flexq_gemm_wrapper.cu:21-97; FT's decoder attention calls it with the packed output of its
- * fused RMSNorm, LlamaV2DecoderSelfAttentionLayer.cc:653).  Where fq_linear_w6ax would fuse its
- * quantizer (decode sizes) the planes are unpacked inside the GEMM's prologue: ONE launch, no
+ * fused RMSNorm, LlamaV2DecoderSelfAttentionLayer.cc:653).  At decode sizes (on the LLaMA shapes M = 1, 2
+ * and M = 4 at K = 4096) the planes are unpacked inside the GEMM's prologue: ONE launch, no
  * scratch.  Otherwise fq_import_ref_x writes xq_buf / xs_buf (fq_planes_act_scratch_bytes: M*K
  * bytes of codes + 2*M*(K/128) of scales, 0 when fused) and fq_gemm_w6ax follows.  Output
  * bit-identical to fq_import_ref_x + fq_gemm_w6ax.  M <= 8 or M % 8 == 0 (the plane layout);

@@ -37,7 +37,7 @@ def planes_case(ops, dev, M, N, K, abits, seed, xraw=None):
     kat_xraw, _, _, wq, xs, ws = kat_operands(M, N, K, abits, seed)
     if xraw is None:
         xraw = kat_xraw
-    xq =((xraw ^ (1 << (abits - 1))) - (1 << (abits - 1))).astype(np.int8)
+    xq = ((xraw ^ (1 << (abits - 1))) - (1 << (abits - 1))).astype(np.int8)
     X = to_dev(oracle.pack_bitplanes(xraw, abits), dev)
     XS = to_dev(oracle.xs_to_ref_dup(xs, M, K), dev)
     pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
@@ -88,7 +88,9 @@ def test_planes_fuse_at_decode_sizes(ops):
     L = _lib.load()
     for (N, K) in [(12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008), (28672, 8192), (8192, 8192)]:
         assert L.fq_planes_act_scratch_bytes(1, N, K) == 0, (N, K)
+    assert L.fq_planes_act_scratch_bytes(4, 4096, 4096) == 0  # 16 pairs per wave: still one launch
     assert L.fq_planes_act_scratch_bytes(1, 8192, 28672) == 28672 + 2 * (28672 // 128)
+    assert L.fq_planes_act_scratch_bytes(8, 4096, 4096) == 8 * 4096 + 2 * 8 * 32
     assert L.fq_planes_act_scratch_bytes(64, 4096, 4096) == 64 * 4096 + 2 * 64 * 32
 
 

@@ -42,7 +42,7 @@ def timed(fn, reps=40):
 
 def main():
     dev = torch.device("cuda:0")
-    for M in (1, 4):
+    for M in [int(v) for v in os.environ.get("PB_M", "1,4").split(",")]:
         for (N, K) in [(12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008)]:
             bits = 6
             nimg = 8
