@@ -1423,240 +1423,6 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     }
 }
 
-// 32 x 32 x 32 core at M >= 2048 (development A/B switch until it is measured faster)
-#ifndef FQ_PB32
-#define FQ_PB32 0
-#endif
-#ifndef FQ_PB32_ACC1
-#define FQ_PB32_ACC1 0
-#endif
-// The same 256 x 256 workgroup tile, stages, DMA split and block order on the 32 x 32 x 32 int8
-// MFMA: a wave's 128 x 64 tile is 4 x 2 blocks of 32 x 32, four chained k-steps of 32 per group
-// (32 MFMA issues per wave and group instead of 64; each issue holds the SIMD's vector issue the
-// same ~8 cycles whatever its size, MI355X_MICROARCH.md).  Operand maps (cdna_hip_programming.md
-// §3, i8 = the bf16 map at 2x K): lane l, r = l & 31, h = l >> 5 holds A[row r][k = 16 h + j] and
-// B[k = 16 h + j][col r], j = 0..15; D: col = r, row = (v & 3) + 8 (v >> 2) + 4 h, v = 0..15.  The
-// weights are the A operand, so a lane owns ONE activation row m and four runs of 4 consecutive
-// columns 8 s + 4 h (s = 0..3) per block.  Group k-step q = 0..3 covers k = 32 q + 16 h + j: in the
-// unpacked-B stage ([tile][64-k step][lane][16 B]) that is 64-k step q >> 1, lane (r & 15) +
-// 16 (2 (q & 1) + h) of tile 2 cb + (r >> 4); in the swizzled A rows, chunk 2 q + h.  The dequant
-// per output and group is the reference's order (flexq_bmma_kernel.h:359-373) as in the kernels
-// above; outputs and accumulators bit-identical to them.
-template <bool DBG, bool XSF = false>
-__global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big32_kernel(
-    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
-    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu) {
-    extern __shared__ __attribute__((aligned(16))) char pb_smem[];
-    char *sa = pb_smem, *sbu = pb_smem + 2 * PB_ASTAGE;
-    const int G = K / FQ_GROUP, NT = (N + 15) / 16;
-    const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wid >> 2, wn = wid & 3;  // 2 x 4 waves of 128 rows x 64 columns
-
-    const int nbm = (M + PB_BM - 1) / PB_BM, nbn = (NT + PB_TILES - 1) / PB_TILES, nwg = nbm * nbn;
-    const int bid = blockIdx.x, xcd = bid % 8, q8 = nwg / 8, rr = nwg % 8;
-    const int lid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + bid / 8;
-    const int span = 8 * nbn, first = (lid / span) * 8;
-    const int gsz = nbm - first < 8 ? nbm - first : 8;
-    const int bm = first + (lid % span) % gsz, bn = (lid % span) / gsz;
-    const int m0 = bm * PB_BM, t0 = bn * PB_TILES;
-
-    // DMA as fq_gemm_prefill_big_kernel (waves 4-7 issue, priority 1), the A rows and unpacked B
-    // through buffer resources: one 32-bit lane offset each, the row / tile / group parts in the
-    // scalar offset, rows >= M and tiles >= NT out of range (read as zero, never stored).  Fewer
-    // live address registers than per-piece 64-bit pointers: the 32 x 32 core needs them.
-    const bool dmaw = wid >= 4;
-    if (dmaw) __builtin_amdgcn_s_setprio(1);
-    const int v4 = wid & 3;
-    const int swz = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;
-    const int srow = 64 * v4 + lane;
-    const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)xq, (short)0, M * K, 0x00020000);
-    const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void *)wu, (short)0, NT * G * 2048, 0x00020000);
-    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc((void *)xs, (short)0, G * M * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void *)wsb, (short)0, NT * G * 32, 0x00020000);
-    const uint32_t xoff = (uint32_t)(m0 + 64 * v4 + (lane >> 3)) * (uint32_t)K + swz, boff = lane * 16;
-    const uint32_t soff = XSF ? (uint32_t)(m0 + 8 * lane) * 2 : (uint32_t)(m0 + srow < M ? m0 + srow : M - 1) * 2;
-    const uint32_t woff = (uint32_t)(wt * G * 16 + 8 * (lane & 1)) * 2;
-    auto stage = [&](int g, int slot) {
-        if (!dmaw) return;
-        char *buf = sa + slot * PB_ASTAGE;
-        // the scales first: should the compiler reload an offset from scratch, its vmcnt(0) then
-        // waits for the previous stage only (already landed), not for this stage's pieces
-        if (XSF) {
-            if (wid == 5 && lane < 32)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(sr, LDS_PTR(buf + PB_XS_OFF), 16, soff, (uint32_t)(g * M * 2), 0, 0);
-        } else {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(sr, LDS_PTR(buf + PB_XS_OFF + 64 * v4 * 4), 2, soff, (uint32_t)(g * M * 2), 0, 0);
-        }
-        if (wid == 4 && lane < 32)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, LDS_PTR(buf + PB_WS_OFF), 16, woff, (uint32_t)(g * 32), 0, 0);
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, LDS_PTR(buf + (64 * v4 + 8 * i) * FQ_GROUP), 16, xoff,
-                                                     (uint32_t)(8 * i * K + g * FQ_GROUP), 0, 0);
-        char *bdst = sbu + slot * PB_BSTAGE + 4 * v4 * 2048;
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int k = 0; k < 2; k++)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(br, LDS_PTR(bdst + t * 2048 + k * 1024), 16, boff,
-                                                         (uint32_t)(((t0 + 4 * v4 + t) * G + g) * 2048 + k * 1024), 0, 0);
-    };
-
-    const int r32 = lane & 31, h = lane >> 5;
-    const uint32_t la = lds_addr(sa), lbu = lds_addr(sbu);
-    const int arow = wm * 128 + r32;  // + 32 rb
-    // A: one base per k-step q (the chunk XOR is per lane), row blocks 32 rows = 4 KiB apart
-    uint32_t a_off[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) a_off[q] = arow * FQ_GROUP + xswz(arow, 2 * q + h);
-    const uint32_t x_off = PB_XS_OFF + arow * (XSF ? 2 : 4);
-    const uint32_t w_off = PB_WS_OFF + (wn * 64 + 4 * h) * 2;                        // + 64 cb + 16 s
-    const uint32_t b_off = (wn * 4 + (r32 >> 4)) * 2048 + ((r32 & 15) + 16 * h) * 16;  // + 4096 cb + 512 q
-
-    float out[4][2][16];  // [rb][cb][v]: row 32 rb + r, column 32 cb + (v & 3) + 8 (v >> 2) + 4 h
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-#pragma unroll
-            for (int v = 0; v < 16; v++) out[i][j][v] = 0.f;
-
-    stage(0, 0);
-    __builtin_amdgcn_s_waitcnt(vmcnt_only(0));
-    for (int g = 0; g < G; g++) {
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        stage(g + 1 < G ? g + 1 : G - 1, (g + 1) & 1);
-        const uint32_t ab = la + (g & 1) * PB_ASTAGE, bb = lbu + (g & 1) * PB_BSTAGE + b_off;
-        v4i b[2][4];   // [cb][q]
-        v2u wv[2][4];  // [cb][s]: the w-scales of columns 32 cb + 8 s + 4 h .. + 3
-        v4i a[2][4];   // [rb & 1][q]
-        uint32_t xv[2];
-#define FQ_PB32_B(cb)                                              \
-        b[cb][0] = ds_read_b128_at<(cb) * 4096>(bb);                \
-        b[cb][1] = ds_read_b128_at<(cb) * 4096 + 512>(bb);          \
-        b[cb][2] = ds_read_b128_at<(cb) * 4096 + 1024>(bb);         \
-        b[cb][3] = ds_read_b128_at<(cb) * 4096 + 1536>(bb);         \
-        wv[cb][0] = ds_read_b64_at<(cb) * 64>(ab + w_off);          \
-        wv[cb][1] = ds_read_b64_at<(cb) * 64 + 16>(ab + w_off);     \
-        wv[cb][2] = ds_read_b64_at<(cb) * 64 + 32>(ab + w_off);     \
-        wv[cb][3] = ds_read_b64_at<(cb) * 64 + 48>(ab + w_off);
-        FQ_PB32_B(0) FQ_PB32_B(1)
-#undef FQ_PB32_B
-        auto read_a = [&](int rb) {  // row block rb into slot rb & 1 (5 reads)
-            const int c = rb & 1;
-#pragma unroll
-            for (int q = 0; q < 4; q++) a[c][q] = ds_read_b128(ab + a_off[q] + rb * 32 * FQ_GROUP);
-            xv[c] = XSF ? ds_read_u16(ab + x_off + rb * 64) : ds_read_b32(ab + x_off + rb * 128);
-        };
-        read_a(0);
-        v16i accq[2];
-        __half2 x2s[2];  // the x-scale pair of row blocks rb (even / odd), kept past the slot's reuse
-        auto dequant = [&](const v16i &acc, int rb, int cb) {
-            float *o = out[rb][cb];
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const uint32_t w01 = wv[cb][s][0], w23 = wv[cb][s][1];
-                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2s[rb & 1]);  // fp16-rounded
-                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2s[rb & 1]);  // scale product
-                o[4 * s + 0] = fmaf((float)acc[4 * s + 0], __low2float(p01), o[4 * s + 0]);
-                o[4 * s + 1] = fmaf((float)acc[4 * s + 1], __high2float(p01), o[4 * s + 1]);
-                o[4 * s + 2] = fmaf((float)acc[4 * s + 2], __low2float(p23), o[4 * s + 2]);
-                o[4 * s + 3] = fmaf((float)acc[4 * s + 3], __high2float(p23), o[4 * s + 3]);
-            }
-            if (DBG) {
-                const int m = m0 + arow + rb * 32;
-#pragma unroll
-                for (int v = 0; v < 16; v++) {
-                    const int n = (t0 + wn * 4) * 16 + 32 * cb + (v & 3) + 8 * (v >> 2) + 4 * h;
-                    if (m < M && n < N) acc_dbg[((size_t)m * N + n) * G + g] = acc[v] >> 2;
-                }
-            }
-        };
-        // Blocks j = (rb, cb) in order, the dequant of block j - 1 after the MFMAs of block j.
-#pragma unroll
-        for (int j = 0; j <= 8; j++) {
-            if (j < 8) {
-                const int rb = j >> 1, cb = j & 1, c = rb & 1;
-                if (cb == 0) {
-                    // row block rb + 1 into the other slot (row block rb - 1's MFMAs are issued; its
-                    // x-scale pair lives on in x2s), then wait for row block rb (and B, w-scales)
-                    if (rb + 1 < 4) {
-                        read_a(rb + 1);
-                        asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(a[c][2]), "+v"(a[c][3]),
-                                     "+v"(xv[c]), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[0][3]),
-                                     "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2]), "+v"(b[1][3]), "+v"(wv[0][0]),
-                                     "+v"(wv[0][1]), "+v"(wv[0][2]), "+v"(wv[0][3]), "+v"(wv[1][0]), "+v"(wv[1][1]),
-                                     "+v"(wv[1][2]), "+v"(wv[1][3]));
-                    } else {
-                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(a[c][2]), "+v"(a[c][3]),
-                                     "+v"(xv[c]));
-                    }
-                    const uint32_t x2u = __builtin_amdgcn_perm(xv[c], xv[c], 0x01000100u);  // half2(xs, xs)
-                    x2s[rb & 1] = *reinterpret_cast<const __half2 *>(&x2u);
-                }
-                v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[cb][0], a[c][0], v16i{}, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[cb][1], a[c][1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[cb][2], a[c][2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[cb][3], a[c][3], acc, 0, 0, 0);
-                if (FQ_PB32_ACC1) {  // (development: one accumulator set, dequant right behind its MFMAs)
-                    __builtin_amdgcn_sched_barrier(0);
-                    dequant(acc, rb, cb);
-                } else {
-                    accq[j & 1] = acc;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (!FQ_PB32_ACC1 && j > 0) dequant(accq[(j - 1) & 1], (j - 1) >> 1, (j - 1) & 1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt(vmcnt_only(0));  // stage g + 1 landed
-    }
-
-    // Epilogue: per block and run pair (2u, 2u + 1), one v_permlane32_swap per dword gives lanes
-    // h = 0 the 8 consecutive columns of run 2u and lanes h = 1 those of run 2u + 1: 16-byte stores.
-    const bool vec8 = (N & 7) == 0;
-#pragma unroll
-    for (int rb = 0; rb < 4; rb++) {
-        const int m = m0 + arow + rb * 32;
-#pragma unroll
-        for (int cb = 0; cb < 2; cb++) {
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                uint32_t pk[2][2];  // [run 2u + e][dword]
-#pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    const float *o = out[rb][cb] + 4 * (2 * u + e);
-                    pk[e][0] = (uint32_t)f2h(o[0] * 0.25f) | ((uint32_t)f2h(o[1] * 0.25f) << 16);
-                    pk[e][1] = (uint32_t)f2h(o[2] * 0.25f) | ((uint32_t)f2h(o[3] * 0.25f) << 16);
-                }
-#pragma unroll
-                for (int w = 0; w < 2; w++) {
-                    const auto r = __builtin_amdgcn_permlane32_swap(pk[0][w], pk[1][w], false, false);
-                    pk[0][w] = r[0];
-                    pk[1][w] = r[1];
-                }
-                const int n = (t0 + wn * 4) * 16 + 32 * cb + 8 * (2 * u + h);
-                if (m < M) {
-                    uint16_t *dst = d + (size_t)m * N + n;
-                    if (vec8 && n + 7 < N) {
-                        *reinterpret_cast<uint4 *>(dst) = make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 8; r++)
-                            if (n + r < N) dst[r] = (uint16_t)(pk[r >> 2][(r >> 1) & 1] >> (16 * (r & 1)));
-                    }
-                }
-            }
-        }
-    }
-}
-
 // =============================================================================================
 // Host side: plan + launch
 // =============================================================================================
@@ -2204,14 +1970,8 @@ fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_
             return FQ_OK;
         }
 #define FQ_BIG(dbg, xf)                                                                                  \
-        do {                                                                                                 \
-        if (FQ_PB32 && (size_t)M * K < (1u << 31) && (size_t)NT * 16 * K < (1u << 31))                      \
-            hipLaunchKernelGGL((fq_gemm_prefill_big32_kernel<dbg, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
-                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);  \
-        else                                                                                                 \
-            hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
-                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu); \
-        } while (0)
+        hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
+                           xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu)
         if (acc_dbg) {
             if (xsf) FQ_BIG(true, true); else FQ_BIG(true, false);
         } else {
