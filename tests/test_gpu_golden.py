@@ -169,7 +169,17 @@ def linear_bound(x16, w16, xs_g, ws_g, abits):
 def test_quant_linear_vs_reference_fixture(dev, tag, M, K, N, abits, surface):
     """C1 (M = 1, K = N = 4096, W6A6) and the M = 16 W6A8 down_proj case against the reference's
     QuantLinear.forward outputs: through fq_linear_w6ax directly and through the operator surface
-    (QuantLinear(...).to_engine()), the reference flow's weight_quant_inplace included."""
+    (QuantLinear(...).to_engine()), the reference flow's weight_quant_inplace included.
+
+    Why the bound below is not a plain 1e-3 relative one: north_star's 1e-3 relative holds
+    engine against engine (test_gpu_kernels.py, oracle.gemm_tolerance).  The reference's Python
+    fake-quant rounds half-to-even (torch.round) where its own CUDA engine rounds half away from
+    zero (roundf, bit_packing.cu:125-164), so the two reference paths already disagree on 0.2-1.2 %
+    of the activation codes; measured on these fixtures (the engine oracle's outputs against the
+    fixture's y), the median output differs by 1.2 % (M = 1) / 0.35 % (M = 16 A8) relative and
+    only 6 % / 19 % of outputs are within 1e-3.  The assertions therefore hold the HIP output to
+    the exact bound those code differences imply, plus the fp16 noise of the reference's own
+    CPU F.linear."""
     g = gold(f"linear_fp16_{tag}.npz")
     x16 = act_input(M, K, seed=2).astype(np.float16)
     w16 = weight_input(N, K, seed=1).astype(np.float16)
