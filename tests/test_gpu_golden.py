@@ -171,15 +171,17 @@ def test_quant_linear_vs_reference_fixture(dev, tag, M, K, N, abits, surface):
     QuantLinear.forward outputs: through fq_linear_w6ax directly and through the operator surface
     (QuantLinear(...).to_engine()), the reference flow's weight_quant_inplace included.
 
-    Why the bound below is not a plain 1e-3 relative one: north_star's 1e-3 relative holds
-    engine against engine (test_gpu_kernels.py, oracle.gemm_tolerance).  The reference's Python
-    fake-quant rounds half-to-even (torch.round) where its own CUDA engine rounds half away from
-    zero (roundf, bit_packing.cu:125-164), so the two reference paths already disagree on 0.2-1.2 %
-    of the activation codes; measured on these fixtures (the engine oracle's outputs against the
-    fixture's y), the median output differs by 1.2 % (M = 1) / 0.35 % (M = 16 A8) relative and
-    only 6 % / 19 % of outputs are within 1e-3.  The assertions therefore hold the HIP output to
-    the exact bound those code differences imply, plus the fp16 noise of the reference's own
-    CPU F.linear."""
+    Why the per-output bound against the fixture's y is not a plain 1e-3 relative one: the
+    reference's own y (fp16 F.linear on the CPU) is itself far from the exact product of its
+    dequantized operands -- measured on these fixtures, median 1.2 % (M = 1) / 0.35 % (M = 16 A8)
+    relative, only 5 % / 18 % of outputs within 1e-3 -- while the engine's outputs sit at a median
+    3e-4 of it (86 % within 1e-3; the rest is the fp16-rounded scale product of the engine's own
+    epilogue, flexq_bmma_kernel.h:359-373, where outputs cancel).  The Python rule (torch.round,
+    half to even) and the engine rule (roundf, half away) also part on a few codes (the mask
+    below).  So: each output within the exact bound the code differences imply plus the fp16 noise
+    of the reference's own F.linear, and north_star's 1e-3 relative on the median against the
+    exact product; engine against engine it holds per output (test_gpu_kernels.py,
+    oracle.gemm_tolerance)."""
     g = gold(f"linear_fp16_{tag}.npz")
     x16 = act_input(M, K, seed=2).astype(np.float16)
     w16 = weight_input(N, K, seed=1).astype(np.float16)
@@ -218,6 +220,8 @@ def test_quant_linear_vs_reference_fixture(dev, tag, M, K, N, abits, surface):
     assert np.all(np.abs(gy - y_exact) <= 1e-3 * absdot)
     # ... the HIP output within the code-difference bound (+ fp16 output rounding) of it ...
     assert np.all(np.abs(y - y_exact) <= bound + 2e-4 * absdot + 1e-3 * np.abs(y_exact))
+    # ... at a median relative error within north_star's 1e-3 of the exact product ...
+    assert np.median(np.abs(y - y_exact) / np.maximum(np.abs(y_exact), 1e-30)) <= 1e-3
     # ... and therefore of the reference's own numbers
     err = np.abs(y - gy)
     assert np.all(err <= bound + 1.2e-3 * absdot + 1e-3 * np.abs(y_exact)), float((err - bound).max())
