@@ -396,18 +396,28 @@ __device__ __forceinline__ void decode_body(
         for (int c = 0; c < xwin && r0 + c < R; c += 8) {
             const int pp = c + (lane >> 3), rg = r0 + pp, q = lane & 7;
             const uint32_t pa = lds_addr(xh_st + pp * 128 + (q >> 1) * 4);
+            const bool a8 = abits == 8;  // wave-uniform: planes 6 and 7 only at A8
             uint32_t w[8];
 #pragma unroll
-            for (int p = 0; p < 8; p++) w[p] = ds_read_b32(pa + p * 16);
+            for (int p = 0; p < 6; p++) w[p] = ds_read_b32(pa + p * 16);
+            if (a8) {
+                w[6] = ds_read_b32(pa + 6 * 16);
+                w[7] = ds_read_b32(pa + 7 * 16);
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]),
                          "+v"(w[5]), "+v"(w[6]), "+v"(w[7])::"memory");
             uint32_t o[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int p = 0; p < 8; p++) {
-                const uint32_t mul = p < abits - 1 ? (1u << p) : (p == abits - 1 ? sgn : 0u);
+            auto plane = [&](int p, uint32_t mul) {
                 const uint32_t h = __builtin_bitreverse32(w[p]) >> (16 * (q & 1));
 #pragma unroll
                 for (int dd = 0; dd < 4; dd++) o[dd] += ((((h >> (4 * dd)) & 15u) * 0x00204081u) & 0x01010101u) * mul;
+            };
+#pragma unroll
+            for (int p = 0; p < 5; p++) plane(p, 1u << p);
+            plane(5, a8 ? 32u : sgn);
+            if (a8) {
+                plane(6, 64u);
+                plane(7, sgn);
             }
             if (pp < xwin && rg < R) {
                 const int j = M == 1 ? rg : rg / M, row = rg - j * M;
