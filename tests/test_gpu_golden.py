@@ -161,7 +161,10 @@ def linear_bound(x16, w16, xs_g, ws_g, abits):
     y_exact = xh @ wh.T
     absdot = np.abs(xh) @ np.abs(wh).T
     bound = np.abs((ref_x - eng_x) * sx) @ np.abs(eng_w * sw).T + np.abs(xh) @ np.abs((ref_w - eng_w) * sw).T
-    return y_exact, absdot, bound
+    # the same product under the engine's activation codes and either weight codes (the C ABI
+    # quantizes W with the engine rule; QuantLinear.to_engine packs the reference's fake-quant W)
+    y_eng = {"c_abi": (eng_x * sx) @ (eng_w * sw).T, "quantlinear": (eng_x * sx) @ wh.T}
+    return y_exact, absdot, bound, y_eng
 
 
 @pytest.mark.parametrize("tag,M,K,N,abits", [("m1", 1, 4096, 4096, 6), ("m16a8", 16, 1024, 256, 8)])
@@ -172,16 +175,15 @@ def test_quant_linear_vs_reference_fixture(dev, tag, M, K, N, abits, surface):
     (QuantLinear(...).to_engine()), the reference flow's weight_quant_inplace included.
 
     Why the per-output bound against the fixture's y is not a plain 1e-3 relative one: the
-    reference's own y (fp16 F.linear on the CPU) is itself far from the exact product of its
-    dequantized operands -- measured on these fixtures, median 1.2 % (M = 1) / 0.35 % (M = 16 A8)
-    relative, only 5 % / 18 % of outputs within 1e-3 -- while the engine's outputs sit at a median
-    3e-4 of it (86 % within 1e-3; the rest is the fp16-rounded scale product of the engine's own
-    epilogue, flexq_bmma_kernel.h:359-373, where outputs cancel).  The Python rule (torch.round,
-    half to even) and the engine rule (roundf, half away) also part on a few codes (the mask
-    below).  So: each output within the exact bound the code differences imply plus the fp16 noise
-    of the reference's own F.linear, and north_star's 1e-3 relative on the median against the
-    exact product; engine against engine it holds per output (test_gpu_kernels.py,
-    oracle.gemm_tolerance)."""
+    reference's fake-quant rounds the fp16-rounded quotient half to even, the engine the fp32
+    quotient half away from zero (bit_packing.cu:125-164), and the two rules part on ~0.3 % of the
+    activation and weight codes here (the mask below).  Measured on these fixtures, those few
+    codes alone move the exact product by a median 1.2 % (M = 1) / 0.35 % (M = 16 A8) -- a
+    difference between the reference's two paths, not an error of either.  So each output is held
+    within the exact bound the code differences imply plus the fp16 noise of the reference's own
+    CPU F.linear, and north_star's 1e-3 relative on the median against the exact product of the
+    codes each side used (the engine ~3.0e-4, the reference's F.linear ~3.3e-4); engine against
+    engine it holds per output (test_gpu_kernels.py, oracle.gemm_tolerance)."""
     g = gold(f"linear_fp16_{tag}.npz")
     x16 = act_input(M, K, seed=2).astype(np.float16)
     w16 = weight_input(N, K, seed=1).astype(np.float16)
@@ -214,14 +216,18 @@ def test_quant_linear_vs_reference_fixture(dev, tag, M, K, N, abits, surface):
     np.testing.assert_array_equal(xs.cpu().numpy().T.reshape(-1).view(np.uint16),
                                   g["x_scale"].reshape(-1).view(np.uint16))
     y = y.cpu().numpy().astype(np.float64)
-    y_exact, absdot, bound = linear_bound(x16, w16, g["x_scale"].reshape(-1), g["w_scale"].reshape(-1), abits)
+    y_exact, absdot, bound, y_eng = linear_bound(x16, w16, g["x_scale"].reshape(-1), g["w_scale"].reshape(-1),
+                                                       abits)
     gy = g["y"].astype(np.float64)
     # the reference's own F.linear (fp16, CPU) sits within its fp16 noise of the exact product ...
     assert np.all(np.abs(gy - y_exact) <= 1e-3 * absdot)
     # ... the HIP output within the code-difference bound (+ fp16 output rounding) of it ...
     assert np.all(np.abs(y - y_exact) <= bound + 2e-4 * absdot + 1e-3 * np.abs(y_exact))
-    # ... at a median relative error within north_star's 1e-3 of the exact product ...
-    assert np.median(np.abs(y - y_exact) / np.maximum(np.abs(y_exact), 1e-30)) <= 1e-3
+    # ... at a median relative error within north_star's 1e-3 of the exact product of its own codes
+    # (measured ~3e-4, the same as the reference's fp16 F.linear against the product of its codes) ...
+    y_own = y_eng[surface]
+    assert np.median(np.abs(y - y_own) / np.maximum(np.abs(y_own), 1e-30)) <= 1e-3
+    assert np.median(np.abs(gy - y_exact) / np.maximum(np.abs(y_exact), 1e-30)) <= 1e-3
     # ... and therefore of the reference's own numbers
     err = np.abs(y - gy)
     assert np.all(err <= bound + 1.2e-3 * absdot + 1e-3 * np.abs(y_exact)), float((err - bound).max())
