@@ -1758,10 +1758,13 @@ static fq_status dispatch_decode(const DecodePlan &p, const DecodeArgs &a, hipSt
 
 // The fused one-launch linear is taken when it fits and its modelled cost (in-kernel quantizer
 // redundant across WGs) does not exceed the split plan's (quantize launch + GEMM).
+#ifndef FQ_FUSE_FORCE_M
+#define FQ_FUSE_FORCE_M 0  // (development: fuse whenever it fits for M <= this, A/B tooling)
+#endif
 static bool decode_fuse(int M, int N, int K, DecodePlan *out, int pro = 0) {
     if (M > 32) return false;
     const DecodePlan f = decode_plan(M, N, K, true, pro);
-    if (!f.fits || f.cost4 > decode_plan(M, N, K, false).cost4) return false;
+    if (!f.fits || (M > FQ_FUSE_FORCE_M && f.cost4 > decode_plan(M, N, K, false).cost4)) return false;
     if (out) *out = f;
     return true;
 }
