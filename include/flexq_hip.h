@@ -244,8 +244,10 @@ fq_status fq_gemm_w6ax_planes(const int32_t *x_bitplanes, const uint16_t *x_scal
  * W_BITS = 6) with X_SCALE in the reference's duplicated layout and W_SCALE half[K/128][N]
  * (required).  The first fq_bmma_exec on a state zeroes the scratch's ticket region and imports
  * W + W_SCALE into a weight image inside `scratch` (once: FT loads its weights once, and
- * `prepared` records it; set it back to 0 after rewriting W); every exec imports X from its bit
- * planes and runs fq_gemm_w6ax.  Run the first exec eagerly before capturing a graph.
+ * `prepared` records it; set it back to 0 after rewriting W); every exec runs
+ * fq_gemm_w6ax_planes on X's bit planes (decode sizes: one launch, the planes unpacked inside the
+ * GEMM; otherwise imported into the scratch first).  Run the first exec eagerly before capturing
+ * a graph.
  * fq_bmma_init_image is the fast path for callers that keep the weight image (fq_import_ref_w /
  * fq_pack_w6 output) themselves: no W_SCALE, no image in scratch.  A caller cannot pass one form
  * for the other by accident: the two entry points name the form.
