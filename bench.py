@@ -12,16 +12,16 @@ input, so by default they run as one linear over the concatenated weight image [
 launch), the whole step captured into one HIP graph.
 
 Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself through a child torchrun
-when it is not already under one): by default (`--parallel dp`) every GPU runs the whole stack on
-its own token stream -- decoding sequences are independent units, so they are partitioned over
-the ranks with no data-path collective ("scaling": "weak", `value` = all ranks' tokens per the
-max-over-ranks step time).  The north-star split of the same stack is measured beside it in the
-same line (`tp`: every linear column-parallel over the N GPUs, SURVEY.md §8(e), each rank packs
-and streams only its N/P rows, ONE RCCL all-gather per linear assembles the dequantized fp16
-output over xGMI; total work fixed, strong scaling; `tp_peer_gather`: the all-gather fused into
-the GEMM epilogue), as is BASELINE config C4, the LLaMA-2-70B column-parallel stack
-(`c4_llama2_70b_tp`).  `--parallel tp` makes the column-parallel step the `value` (then
-`replicas` is the section beside it).
+when it is not already under one): by default (`--parallel c4`) `value` is the north-star split,
+BASELINE config C4: the LLaMA-2-70B linear stack with every linear column-parallel over the N GPUs
+(each rank packs and streams only its N/P rows, ONE all-gather per linear
+assembles the dequantized fp16 output over xGMI -- RCCL's all_gather, or the peer-store gather
+fused into the GEMM epilogue when every rank's output is bit-identical to the RCCL run's and it is
+faster); total work fixed, "scaling": "strong".  C4's one-GPU point is the N = 1 line's
+`c4_llama2_70b_1gpu` section (the N = 1 `value` stays BASELINE configs[1], LLaMA-2-7B).  Beside
+it: the same split of the 7B stack (`tp_llama2_7b`, `tp_llama2_7b_peer_gather`) and the 7B stack as
+independent replicas, one token stream per GPU (`replicas`, weak scaling).  `--parallel tp` /
+`--parallel dp` make the 7B split / the replicas the `value` instead.
 
 Output: one JSON line (rank 0) with the metric, the roofline of the dominant kernel (the decode
 linear), the north-star comparison against rocBLAS/hipBLASLt fp16 GEMM, and the CPU baseline (the oracle's restatement of the reference's fake-quant QuantLinear
@@ -186,6 +186,14 @@ def time_graph(g, reps, stream):
 
 
 NORTH_STAR_SHAPES = [(24576, 8192), (8192, 8192), (28672, 8192), (8192, 28672)]  # test_flexq_kernel.sh:25-28
+# the reference's own kernel sweep (engine/test_flexq_kernel.sh:7-39): (model, N, K, abits) at M = 1, 2, 4, 8
+REFERENCE_SWEEP = [("llama_7b", 12288, 4096, 6), ("llama_7b", 4096, 4096, 6), ("llama_7b", 11008, 4096, 6),
+                   ("llama_7b", 4096, 11008, 8), ("llama_30b", 19968, 6656, 6), ("llama_30b", 6656, 6656, 6),
+                   ("llama_30b", 17920, 6656, 6), ("llama_30b", 6656, 17920, 8), ("llama_2_13b", 15360, 5120, 6),
+                   ("llama_2_13b", 5120, 5120, 6), ("llama_2_13b", 13824, 5120, 6), ("llama_2_13b", 5120, 13824, 8),
+                   ("llama_2_70b", 24576, 8192, 6), ("llama_2_70b", 8192, 8192, 6), ("llama_2_70b", 28672, 8192, 6),
+                   ("llama_2_70b", 8192, 28672, 8), ("opt_30b", 21504, 7168, 6), ("opt_30b", 7168, 7168, 6),
+                   ("opt_30b", 28672, 7168, 6), ("opt_30b", 7168, 28672, 8)]
 
 
 def int8_vendor_us(N, K, M, dev, g, s, reps):
@@ -253,6 +261,72 @@ def fp16_compare(shapes, M, abits, dev, reps=20, int8=False):
             torch.cuda.synchronize()
         out.append(row)
     return out
+
+
+def reference_sweep(dev, Ms=(1, 2, 4, 8), reps=10, budget=512 * 2**20):
+    """README.md:189's comparison on the reference's own sweep (engine/test_flexq_kernel.sh:7-39): every
+    (N, K, abits) shape of LLaMA-7B, LLaMA-30B, LLaMA-2-13B, LLaMA-2-70B and OPT-30B at M = 1, 2, 4, 8.
+    Per shape and M, graph-timed over rotating weight copies (>= `budget` bytes, beyond the MALL):
+      * w6_gemm_us: the W6Ax GEMM on pre-quantized activations (what test_bgemm_kernel times:
+        benchmark<> runs exec_fn on packed X, test/test_kernel.h:131-142);
+      * w6_linear_us: the whole linear, dynamic activation quantization included;
+      * fp16_us: torch F.linear fp16 (hipBLASLt / rocBLAS), the north-star denominator;
+      * int8_us: the vendor int8 GEMM torch._int_mm (the reference's cuBLAS W8A8 baseline,
+        engine/test_cublas_kernel.cu:122-133), at the smallest M >= 17 it accepts (one value per shape).
+    Averages per M in README.md:189's form: the arithmetic mean of the per-shape speedups."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    s = torch.cuda.Stream(dev)
+    rows, by_m = [], {m: {"vs_int8": [], "vs_fp16": [], "linear_vs_int8": []} for m in Ms}
+    for (model, N, K, ab) in REFERENCE_SWEEP:
+        c16 = max(2, -(-budget // (2 * N * K)))
+        c6 = max(2, -(-budget // (N * K * 3 // 4)))
+        w16 = [torch.randn((N, K), dtype=torch.float16, device=dev, generator=g) * 0.02 for _ in range(c16)]
+        w6 = [ops.pack_w6(torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g),
+                          (torch.rand((K // GROUP, N), device=dev, generator=g) * 0.02).half()) for _ in range(c6)]
+        ti, mi = int8_vendor_us(N, K, 1, dev, g, s, reps)
+        for M in Ms:
+            x = torch.randn((M, K), dtype=torch.float16, device=dev, generator=g)
+            xq, xs = ops.quantize_act(x, ab)
+            y16 = torch.empty((M, N), dtype=torch.float16, device=dev)
+            y6 = torch.empty((M, N), dtype=torch.float16, device=dev)
+            with torch.cuda.stream(s):
+                torch.nn.functional.linear(x, w16[0], out=y16)
+                ops.linear_w6ax(x, w6[0], N, ab, out=y6)
+                ops.gemm_w6ax(xq, xs, w6[0], N, ab, out=y6)
+            torch.cuda.synchronize()
+            t = {}
+            for key, fn in (("fp16", lambda: [torch.nn.functional.linear(x, w16[i % c16], out=y16) for i in range(reps)]),
+                            ("lin", lambda: [ops.linear_w6ax(x, w6[i % c6], N, ab, out=y6) for i in range(reps)]),
+                            ("gemm", lambda: [ops.gemm_w6ax(xq, xs, w6[i % c6], N, ab, out=y6) for i in range(reps)])):
+                gr = capture(fn, s)
+                gr.replay()
+                torch.cuda.synchronize()
+                t[key] = time_graph(gr, 3, s) / (3 * reps)
+                del gr
+            row = {"model": model, "M": M, "N": N, "K": K, "abits": ab, "w6_gemm_us": round(t["gemm"] * 1e6, 2),
+                   "w6_linear_us": round(t["lin"] * 1e6, 2), "fp16_us": round(t["fp16"] * 1e6, 2),
+                   "speedup_vs_fp16": round(t["fp16"] / t["gemm"], 3)}
+            by_m[M]["vs_fp16"].append(t["fp16"] / t["gemm"])
+            if ti is not None:
+                row.update(int8_us=round(ti * 1e6, 2), int8_M=mi, speedup_vs_int8=round(ti / t["gemm"], 3),
+                           linear_speedup_vs_int8=round(ti / t["lin"], 3))
+                by_m[M]["vs_int8"].append(ti / t["gemm"])
+                by_m[M]["linear_vs_int8"].append(ti / t["lin"])
+            rows.append(row)
+        del w16, w6
+        torch.cuda.empty_cache()
+    mean = lambda v: round(float(np.mean(v)), 3) if v else None  # noqa: E731
+    return {"what": "README.md:189's comparison over the reference's own kernel sweep (engine/test_flexq_kernel.sh:"
+                    "7-39: LLaMA-7B, LLaMA-30B, LLaMA-2-13B, LLaMA-2-70B, OPT-30B; W6A8 down shapes) at M = 1, 2, 4, "
+                    "8: the W6Ax GEMM on pre-quantized activations (as test_bgemm_kernel times it) vs the vendor "
+                    "int8 GEMM torch._int_mm (the reference's cuBLAS W8A8 baseline; run at the smallest M it "
+                    "accepts, int8_M) and vs hipBLASLt fp16 F.linear; graph-timed over rotating weight copies",
+            "reference_published": {"vs_cublas_w8a8_avg": {"1": 1.78, "4": 1.81, "8": 1.82},
+                                    "hardware": "NVIDIA A6000-class (sm_86), README.md:189"},
+            "avg_speedup_vs_int8_by_M": {str(m): mean(v["vs_int8"]) for m, v in by_m.items()},
+            "avg_linear_speedup_vs_int8_by_M": {str(m): mean(v["linear_vs_int8"]) for m, v in by_m.items()},
+            "avg_speedup_vs_fp16_by_M": {str(m): mean(v["vs_fp16"]) for m, v in by_m.items()},
+            "shapes": rows}
 
 
 def pmc_traffic(config, merge):
@@ -325,7 +399,8 @@ def cpu_baseline(budget_s=15.0, lins=None, M=1):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fq_oracle as oracle  # bench's cpu_baseline leg only
     # the GPU box exports OMP_NUM_THREADS = its CPU share (os.cpu_count() reports the whole host)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    quota = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    threads = quota or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
     lins = lins or CONFIGS["llama2-7b-m1"][2]
     rows = min(M, 64)
@@ -355,6 +430,9 @@ def cpu_baseline(budget_s=15.0, lins=None, M=1):
                 sample=f"{sample}: {pre_layers} layers in {pre_dt:.1f} s with pre-quantized weights",
                 tok_per_s=rows * pre_layers / pre_dt / 32,
                 cpu_model=cpu_model(), os_cpu_count=os.cpu_count(), torch_threads=torch.get_num_threads(),
+                cores_reason=("all of this process's CPU share: the GPU lease exports OMP_NUM_THREADS=%d (its CPU "
+                              "quota; os.cpu_count() reports the whole %s-CPU host, shared with other leases)"
+                              % (quota, os.cpu_count()) if quota else "os.cpu_count(): no CPU quota exported"),
                 variants={
                     "prequantized_weights": dict(value=pre, tok_per_s=rows * pre_layers / pre_dt / 32,
                                                  layers=pre_layers, seconds=round(pre_dt, 2)),
@@ -689,11 +767,13 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-fp16-compare", action="store_true", help="skip the rocBLAS fp16 comparison")
     ap.add_argument("--no-calibrate", action="store_true", help="skip the on-box HBM / MFMA peak calibration")
-    ap.add_argument("--parallel", choices=["dp", "tp"], default="dp",
-                    help="N > 1, what `value` measures: dp (default) = independent replicas, one token stream "
-                         "per GPU, no data-path collective (weak scaling); tp = every linear column-sharded over "
-                         "the N GPUs + one all-gather per linear, total work fixed (strong scaling, SURVEY.md "
-                         "§8(e)).  The other one is measured beside it in the same line (`tp` / `replicas`)")
+    ap.add_argument("--parallel", choices=["c4", "tp", "dp"], default="c4",
+                    help="N > 1, what `value` measures: c4 (default) = BASELINE config C4, the LLaMA-2-70B stack "
+                         "with every linear column-sharded over the N GPUs + one all-gather per linear (RCCL, or "
+                         "the peer-store gather when bit-identical and faster), total work fixed (strong scaling, "
+                         "SURVEY.md §8(e)); tp = the same split of the --config stack (LLaMA-2-7B); dp = "
+                         "independent replicas of the --config stack, one token stream per GPU (weak scaling).  "
+                         "The others are measured beside it in the same line (`tp_llama2_7b`, `replicas`)")
     ap.add_argument("--no-replicas", action="store_true", help="N > 1, tp: skip the replica (dp) measurement")
     ap.add_argument("--no-tp", action="store_true", help="N > 1, dp: skip the column-parallel (tp) measurement")
     ap.add_argument("--no-peer", action="store_true",
@@ -702,6 +782,8 @@ def main():
                     help="N > 1: skip the LLaMA-2-70B column-parallel measurement (BASELINE config C4)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="N = 1: skip the C3 (batch 16) and C5 (prefill) steps measured beside the headline")
+    ap.add_argument("--no-reference-sweep", action="store_true",
+                    help="N = 1: skip the reference's kernel sweep (engine/test_flexq_kernel.sh, README.md:189's form)")
     ap.add_argument("--no-layers", action="store_true",
                     help="skip the end-to-end decoder-layer comparison against fp16 (M = 1 and 16)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -728,23 +810,27 @@ def main():
     ctx = Ctx(a, rank, world, dev, staged)
 
     cfg = CONFIGS[a.config]
-    layers, M, lins, desc = cfg
+    # N > 1 headline: BASELINE config C4 (the 70B column split) unless --parallel tp / dp; at N = 1 the
+    # --config stack (BASELINE configs[1] by default) with C4's one-GPU point measured beside it
+    c4_head = world > 1 and a.parallel == "c4" and CONFIGS[a.config][1] <= PREFILL_M
+    hcfg = CONFIGS["llama2-70b-m1"] if c4_head else cfg
+    layers, M, lins, desc = hcfg
     merge = not a.no_merge
     launch_lins = launch_list(lins, merge)
-    tp = world if a.parallel == "tp" else 1  # ranks one linear is sharded over
+    tp = world if (a.parallel == "tp" or c4_head) else 1  # ranks one linear is sharded over
     prefill = M > PREFILL_M
     n_lin = layers * len(launch_lins)
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
 
     if tp > 1:
-        r = measure_tp(ctx, cfg, merge, tp, a.steps, a.warmup)
+        r = measure_tp(ctx, hcfg, merge, tp, a.steps, a.warmup)
         # The column-parallel step's all-gather has two implementations: RCCL's all_gather and the
         # peer-store gather fused into the GEMM epilogue.  Both run; the peer one is
         # taken for `value` only when every rank's step output is bit-identical to the RCCL run's,
         # no wait timed out and it is faster (never in the --share-gpu rehearsal).
         gather_impl, r_rccl, peer_sec = "rccl all_gather_into_tensor", r, {}
         if not a.no_peer and M <= PREFILL_M:
-            optional(peer_sec, "p", lambda: measure_tp(ctx, cfg, merge, tp, a.steps, a.warmup, peer=True), ctx)
+            optional(peer_sec, "p", lambda: measure_tp(ctx, hcfg, merge, tp, a.steps, a.warmup, peer=True), ctx)
             rp = peer_sec["p"]
             if "final" in rp:
                 bad = 0.0 if (rp["finite"] and np.array_equal(rp["final"].view(np.uint16),
@@ -813,7 +899,8 @@ def main():
         "outputs_finite": finite,
         "tok_per_s": round(tok_s, 2),
         "config": {
-            "workload": desc + ", dependent linear stack of every decoder layer per step",
+            "workload": ("BASELINE config C4: " if c4_head else "") + desc +
+                        ", dependent linear stack of every decoder layer per step",
             "layers": layers, "batch_M": M,
             "shapes_NxK": [[N, K, ab] for (_, N, K, ab) in lins],
             "parallelism": (f"tp{world}: every linear column-parallel (N/{world} rows per rank) + one "
@@ -869,7 +956,7 @@ def main():
     def tp_summary(rr):
         return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in rr.items()
                 if k not in ("elapsed", "flops_step", "finite", "final")}
-    if world > 1 and tp == 1 and not a.no_tp:
+    if world > 1 and (tp == 1 or c4_head) and not a.no_tp:
         # the north-star split of the same stack, measured beside the replicas: every
         # linear column-parallel over the N GPUs + one RCCL all-gather per linear (strong scaling)
         def tp_rccl():
@@ -879,25 +966,28 @@ def main():
                     "value": round(rr["flops_step"] * a.steps / rr["elapsed"] / 1e12, 4), "unit": "TFLOPS-equiv",
                     "tok_per_s": round(M * a.steps / rr["elapsed"], 2), **tp_summary(rr),
                     "finite": rr["finite"], "hbm_frac_per_rank": round(rr["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
-        optional(res, "tp", tp_rccl, ctx)
+        optional(res, "tp_llama2_7b" if c4_head else "tp", tp_rccl, ctx)
     if tp > 1:
         res["tp"] = tp_summary(r)
         res["tp"]["gather"] = gather_impl
         res["tp"]["rccl_ms_per_step"] = round(r_rccl["ms_per_step"], 4)
         res["tp"]["hbm_frac_per_rank"] = round(r["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)
-        if not a.no_replicas:  # the same model as independent replicas, one token stream per GPU
+        if not a.no_replicas:  # the --config model as independent replicas, one token stream per GPU
+            # (the replicas run the --config stack, 7B by default)
+            flops_step_r = cfg[0] * sum(2.0 * cfg[1] * N * K for (_, N, K, _) in cfg[2])
+
             def replicas():
                 stack = build_stack(cfg, rank, 1, dev, merge)
-                replay = ctx.prepare(lambda: run_step(stack, M, 1), not a.no_graph)
+                replay = ctx.prepare(lambda: run_step(stack, cfg[1], 1), not a.no_graph)
                 el_dp, _ = ctx.timed(replay, a.steps, a.warmup)
                 del stack, replay
                 torch.cuda.empty_cache()
-                return {"what": f"dp{world}: the whole model on every GPU, independent token streams, "
+                return {"what": f"dp{world}: the whole {a.config} model on every GPU, independent token streams, "
                                 "no data-path collective (weak scaling)",
-                        "value": round(world * flops_step * a.steps / el_dp / 1e12, 4),
-                        "tok_per_s": round(world * M * a.steps / el_dp, 2),
+                        "value": round(world * flops_step_r * a.steps / el_dp / 1e12, 4),
+                        "tok_per_s": round(world * cfg[1] * a.steps / el_dp, 2),
                         "ms_per_step": round(el_dp / a.steps * 1e3, 4)}
-            need = cfg[0] * sum(ops.packed_w_bytes(N, K) for (_, N, K, _) in launch_lins)
+            need = cfg[0] * sum(ops.packed_w_bytes(N, K) for (_, N, K, _) in launch_list(cfg[2], merge))
             optional(res, "replicas", replicas, ctx, need_bytes=need)
     if world > 1:
         if not a.no_peer and M <= 32:  # the all-gather fused into the GEMM epilogue
@@ -912,8 +1002,8 @@ def main():
                         "gemm_only_ms_per_step": round(rp["gemm_only_ms_per_step"], 4),
                         "finite": rp["finite"], "graph": rp["graph"]}
             rp = peer_sec.get("p") if tp > 1 else None
-            if tp == 1 and not a.no_tp:
-                optional(res, "tp_peer_gather", lambda: tp_peer(cfg), ctx)
+            if (tp == 1 or c4_head) and not a.no_tp:
+                optional(res, "tp_llama2_7b_peer_gather" if c4_head else "tp_peer_gather", lambda: tp_peer(cfg), ctx)
             if rp is not None and "final" in rp:
                 res["tp_peer_gather"] = {
                     "what": "the same column-parallel stack, each all-gather fused into its GEMM's epilogue: peer "
@@ -925,9 +1015,9 @@ def main():
                     "bit_identical_to_rccl": rp["bit_identical_to_rccl"], "graph": rp["graph"]}
             elif rp is not None:
                 res["tp_peer_gather"] = rp
-            if not a.no_c4 and a.config != "llama2-70b-m1":
+            if not a.no_c4 and a.config != "llama2-70b-m1" and not c4_head:
                 optional(res, "c4_llama2_70b_tp_peer_gather", lambda: tp_peer(CONFIGS["llama2-70b-m1"]), ctx)
-        if not a.no_c4 and a.config != "llama2-70b-m1" and not prefill:
+        if not a.no_c4 and a.config != "llama2-70b-m1" and not prefill and not c4_head:
             def c4_tp():
                 c4 = CONFIGS["llama2-70b-m1"]
                 rc = measure_tp(ctx, c4, merge, world, max(2, a.steps // 2), max(1, a.warmup // 2))
@@ -942,9 +1032,16 @@ def main():
             optional(res, "c4_llama2_70b_tp", c4_tp, ctx)
     if world == 1 and not a.no_extra_configs:  # the other single-GPU BASELINE configs, same run
         for key, name, st, wu in (("c3_llama2_7b_m16", "llama2-7b-m16", 10, 3),
-                                  ("c5_llama3_8b_prefill", "llama3-8b-prefill", 2, 1)):
+                                  ("c5_llama3_8b_prefill", "llama3-8b-prefill", 2, 1),
+                                  ("c4_llama2_70b_1gpu", "llama2-70b-m1", 10, 3)):
             if name != a.config:
-                optional(res, key, lambda name=name, st=st, wu=wu: measure_single(ctx, name, merge, st, wu), ctx)
+                need = CONFIGS[name][0] * sum(ops.packed_w_bytes(N, K) for (_, N, K, _) in
+                                              launch_list(CONFIGS[name][2], merge))
+                optional(res, key, lambda name=name, st=st, wu=wu: measure_single(ctx, name, merge, st, wu), ctx,
+                         need_bytes=need)
+        if res.get("c4_llama2_70b_1gpu", {}).get("value"):
+            res["c4_llama2_70b_1gpu"]["note"] = ("C4's one-GPU point: bench.py --gpus N (N > 1) reports C4 split "
+                                                 "over the N GPUs as `value`")
     if not a.no_layers and not prefill and a.config.startswith("llama2-7b"):
         optional(res, "decoder_layers_e2e", lambda: {
             "what": f"LLaMA-2-7B decoder layers end to end (32 layers; RMSNorm, qkv, o, gate_up, SiLU*up, down, "
@@ -980,6 +1077,8 @@ def main():
                 "llama2_70b_m1": cmp_ns[1], "llama2_70b_m1_geomean_speedup": geo(cmp_ns[1]),
                 "llama2_70b_geomean_speedup_by_M": {str(m): geo(r) for m, r in cmp_ns.items()},
                 "north_star_target": 1.3})
+    if world == 1 and not a.no_reference_sweep and not prefill:
+        optional(res, "vs_reference_sweep", lambda: reference_sweep(dev), ctx)
     if rank == 0 and world == 1 and a.cpu_budget > 0:
         res["cpu_baseline"] = cpu_baseline(a.cpu_budget, lins, M)
     if rank == 0:

@@ -63,12 +63,15 @@ _SIGS = {
     "fq_bmma_image_scratch_bytes": ([I, I, I], SZ),
     "fq_rmsnorm_quantize": ([P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),
     "fq_silu_mul_quantize": ([P, P, I, I, I, I, P, P, P, P], I),
+    "fq_layernorm_quantize": ([P, P, P, P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),
     "fq_linear_w6ax_gather": ([P, I, I, I, I, P, P, P, P, P, SZ, P], I),
     "fq_gather_wait": ([P, P, P], I),
     "fq_rmsnorm_linear_scratch_bytes": ([I, I, I], SZ),
     "fq_silu_linear_scratch_bytes": ([I, I, I], SZ),
     "fq_rmsnorm_linear_w6ax": ([P, P, P, P, ctypes.c_float, I, I, I, I, P, P, P, P, P, SZ, P], I),
     "fq_silu_linear_w6ax": ([P, P, I, I, I, I, I, P, P, P, P, P, SZ, P], I),
+    "fq_layernorm_linear_scratch_bytes": ([I, I, I], SZ),
+    "fq_layernorm_linear_w6ax": ([P, P, P, P, P, P, ctypes.c_float, I, I, I, I, P, P, P, P, P, SZ, P], I),
 }
 
 

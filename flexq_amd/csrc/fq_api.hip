@@ -66,6 +66,12 @@ extern "C" fq_status fq_linear_w6ax_gather(const uint16_t *x, int M, int N, int 
                              workspace_bytes, stream, gather);
 }
 
+static bool overlaps(const void *a, size_t na, const void *b, size_t nb) {
+    if (!a || !b) return false;
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return x < y + nb && y < x + na;
+}
+
 // ---- producers fused into the linear (the caller side of the path) --------
 // One launch at decode sizes (the producer runs in the decode kernel's prologue); otherwise the
 // producer kernel into xq_buf / xs_buf, then the GEMM.  Same bits either way: both run
@@ -76,18 +82,52 @@ extern "C" fq_status fq_rmsnorm_linear_w6ax(const uint16_t *input, const uint16_
                                             void *workspace, size_t workspace_bytes, fq_stream_t stream) {
     if (!residual || !gamma || !w_packed || !d || (input && !residual_out)) return FQ_ERR_NULL;
     if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
-    if (input && residual_out == residual) return FQ_ERR_SHAPE;  // other workgroups still read it
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     const uintptr_t al = (uintptr_t)residual | (uintptr_t)gamma | (uintptr_t)input | (uintptr_t)residual_out;
     if (al & 15) return FQ_ERR_SHAPE;
+    // the one-launch form: workgroup 0 writes residual_out while the others still read the residual,
+    // the input and gamma, so residual_out must overlap none of them (the unfused form would be
+    // alias-safe, but both forms must give the same bits)
+    const size_t rb = (size_t)M * K * 2;
+    if (input && (overlaps(residual_out, rb, residual, rb) || overlaps(residual_out, rb, input, rb) ||
+                  overlaps(residual_out, rb, gamma, (size_t)K * 2)))
+        return FQ_ERR_SHAPE;
     bool launched = false;
-    const DecodePro pro = {input, gamma, residual_out, eps, K};
+    const DecodePro pro = {input, gamma, residual_out, eps, K, nullptr, nullptr};
     fq_status st = fq_decode_linear_pro(1, residual, pro, M, N, K, abits, w_packed, d, workspace, workspace_bytes,
                                         (hipStream_t)stream, &launched);
     if (launched || st != FQ_OK) return st;
     if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
     st = fq_rmsnorm_quantize_to(input, residual, input ? residual_out : nullptr, gamma, eps, M, K, abits, xq_buf,
                                 xs_buf, nullptr, stream);
+    if (st != FQ_OK) return st;
+    return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" fq_status fq_layernorm_linear_w6ax(const uint16_t *input, const uint16_t *residual, const uint16_t *bias,
+                                              uint16_t *residual_out, const uint16_t *gamma, const uint16_t *beta,
+                                              float eps, int M, int N, int K, int abits, const void *w_packed,
+                                              uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
+                                              size_t workspace_bytes, fq_stream_t stream) {
+    if (!residual || !gamma || !w_packed || !d) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    const uintptr_t al = (uintptr_t)residual | (uintptr_t)gamma | (uintptr_t)input | (uintptr_t)residual_out |
+                         (uintptr_t)beta | (uintptr_t)bias;
+    if (al & 15) return FQ_ERR_SHAPE;
+    const size_t rb = (size_t)M * K * 2, vb = (size_t)K * 2;  // (as fq_rmsnorm_linear_w6ax)
+    if (overlaps(residual_out, rb, residual, rb) || overlaps(residual_out, rb, input, rb) ||
+        overlaps(residual_out, rb, gamma, vb) || overlaps(residual_out, rb, beta, vb) ||
+        overlaps(residual_out, rb, bias, vb))
+        return FQ_ERR_SHAPE;
+    bool launched = false;
+    const DecodePro pro = {input, gamma, residual_out, eps, K, beta, bias};
+    fq_status st = fq_decode_linear_pro(4, residual, pro, M, N, K, abits, w_packed, d, workspace, workspace_bytes,
+                                        (hipStream_t)stream, &launched);
+    if (launched || st != FQ_OK) return st;
+    if (!xq_buf || !xs_buf) return FQ_ERR_NULL;
+    st = fq_layernorm_quantize(input, residual, bias, residual_out, gamma, beta, eps, M, K, abits, xq_buf, xs_buf,
+                               nullptr, stream);
     if (st != FQ_OK) return st;
     return fq_gemm_w6ax(xq_buf, xs_buf, w_packed, M, N, K, abits, d, nullptr, workspace, workspace_bytes, stream);
 }
@@ -101,7 +141,7 @@ extern "C" fq_status fq_silu_linear_w6ax(const uint16_t *gate, const uint16_t *u
     if (abits != 6 && abits != 8) return FQ_ERR_BITS;
     if (((uintptr_t)gate | (uintptr_t)up) & 15) return FQ_ERR_SHAPE;
     bool launched = false;
-    const DecodePro pro = {up, nullptr, nullptr, 0.0f, ld};
+    const DecodePro pro = {up, nullptr, nullptr, 0.0f, ld, nullptr, nullptr};
     fq_status st = fq_decode_linear_pro(2, gate, pro, M, N, K, abits, w_packed, d, workspace, workspace_bytes,
                                         (hipStream_t)stream, &launched);
     if (launched || st != FQ_OK) return st;

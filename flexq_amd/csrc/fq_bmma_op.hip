@@ -30,7 +30,14 @@ struct Scratch {
 // Library-owned device memory of the instances: never freed while the process runs (a captured
 // graph bakes these addresses in), superseded buffers retired instead.
 std::mutex g_mu;
-std::map<WeightKey, void *> g_images;
+// an imported weight image, the stream its import was enqueued on and an event recorded behind the
+// import (null when the import was captured into a graph)
+struct Image {
+    void *img;
+    hipStream_t owner;
+    hipEvent_t ready;
+};
+std::map<WeightKey, Image> g_images;
 std::map<hipStream_t, Scratch> g_scratch;
 std::vector<void *> g_retired;
 size_t g_device_bytes = 0;
@@ -68,7 +75,20 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_mu);
     const WeightKey key{a.W, a.W_SCALE, a.N, a.K};
     auto it = g_images.find(key);
-    if (it != g_images.end()) return it->second;
+    if (it != g_images.end()) {
+        // another stream's first use must not overtake the import enqueued on the owner's stream
+        Image &im = it->second;
+        if (im.ready && s != im.owner) {
+            if (hipEventQuery(im.ready) == hipSuccess) {
+                (void)hipEventDestroy(im.ready);
+                im.ready = nullptr;  // the import has completed: no stream needs to wait any more
+            } else if (hipStreamWaitEvent(s, im.ready, 0) != hipSuccess) {
+                report(FQ_ERR_HIP, "FQBMMA exec: ordering against the weight import");
+                return nullptr;
+            }
+        }
+        return im.img;
+    }
     void *img = nullptr;
     const size_t bytes = fq_packed_w_bytes(a.N, a.K);
     if (hipMalloc(&img, bytes) != hipSuccess) {
@@ -81,7 +101,14 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
         (void)hipFree(img);
         return nullptr;
     }
-    g_images[key] = img;
+    hipEvent_t ready = nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
+        hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess && hipEventRecord(ready, s) != hipSuccess) {
+        (void)hipEventDestroy(ready);
+        ready = nullptr;
+    }
+    g_images[key] = Image{img, s, ready};
     g_device_bytes += bytes;
     return img;
 }
@@ -184,7 +211,8 @@ extern "C" int fq_bmma_op_forget_weight(const void *W) {
     int dropped = 0;
     for (auto it = g_images.begin(); it != g_images.end();) {
         if (it->first.W == W) {
-            g_retired.push_back(it->second);  // a captured graph may still read it: never freed
+            g_retired.push_back(it->second.img);  // a captured graph may still read it: never freed
+            if (it->second.ready) (void)hipEventDestroy(it->second.ready);
             it = g_images.erase(it);
             dropped++;
         } else {

@@ -43,12 +43,9 @@ __device__ __forceinline__ int sat_clamp(float v, int lo, int hi) {
 // Returns the fp16 scale bits and the 8 codes packed as little-endian int8 bytes.
 //
 // The 16-lane max runs on DPP (quad_perm xor1/xor2, row_half_mirror, row_mirror: a full max
-// over the 16-lane row without LDS).  The per-element quotient x / s is v_rcp + one exact-FMA
-// Newton step instead of the IEEE division sequence; the codes are identical because x and s are
-// fp16 (11-bit significands): a quotient that is not exactly a half-integer k + 0.5 lies at least
-// 2^-12 relative away from one, far beyond the step's ~2^-23 error, and an exactly representable
-// quotient (ties included) is reproduced exactly by the Newton step.  Non-finite intermediates
-// (s = 0 or inf) take the plain product, which has the IEEE quotient's value class.
+// over the 16-lane row without LDS).  The per-element quotient and its rounding are one fused
+// multiply-add with a biased reciprocal instead of the IEEE division sequence (see the element
+// step below for why the codes are identical).
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -112,33 +109,21 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
     const float maxv = __builtin_isfinite(m1) ? fmaf(fmaf(-m1, fhi, mx), y, m1) : m1;
     const uint16_t sh = f2h(maxv);
     const float r = h2f(sh);
-    const float rc = __builtin_amdgcn_rcpf(r);
-    const v2f r2 = {r, r}, rc2 = {rc, rc};
-    // Newton step unless the scale is 0 / inf (then the plain product has the IEEE quotient's
-    // value class).  A wave-uniform branch: the common case carries no per-element select.
-    const bool newton = __builtin_isfinite(r) && r != 0.0f;
-    v2f q[4];
-    if (__builtin_amdgcn_ballot_w64(!newton) == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {  // packed fp32 math: v_pk_mul_f32 / v_pk_fma_f32
-            const v2f q1 = v[i] * rc2;
-            q[i] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, r2, v[i]), rc2, q1);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const v2f q1 = v[i] * rc2;
-            q[i] = q1;
-            if (newton) q[i] = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, r2, v[i]), rc2, q1);
-        }
-    }
+    // Element step: roundf(RN(x / r)) == trunc(RN(x * rcb + copysign(0.5, x))) with
+    // rcb = RN(v_rcp(r) * (1 + 2^-20)), one fused multiply-add per element.  x and r are fp16,
+    // so a quotient that is not an exact tie k + 0.5 lies far beyond the reciprocal's error from
+    // one, and the 2^-20 bias carries an exact tie across the truncation boundary.  Exhaustive
+    // over every fp16 absmax and element, both bit widths, the reciprocal off by up to 4 ulp
+    // (oracle/fq_oracle.c fqo_check_quant_fma, tests/test_oracle.py).  r = 0 (an all-zero group)
+    // gives 0 * inf = NaN and r = inf gives +-0.5: code 0, as the IEEE quotient's class does; the
+    // truncating, saturating v_cvt_i32_f32 maps NaN to 0 and +-inf to the int range.
+    const float rcb = __builtin_amdgcn_rcpf(r) * (1.0f + 0x1p-20f);
+    const v2f rcb2 = {rcb, rcb};
     int c[8];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        // roundf = trunc(q + copysign(0.5, q)) here: q is either an exact half-integer or at
-        // least 2^-12 (relative) away from one, so the addition cannot cross an integer; the
-        // truncating, saturating v_cvt_i32_f32 then also maps +-inf to the int range, NaN to 0.
-        const v2f t = q[i] + v2f{__builtin_copysignf(0.5f, q[i].x), __builtin_copysignf(0.5f, q[i].y)};
+    for (int i = 0; i < 4; i++) {  // packed fp32: v_pk_fma_f32
+        const v2f hs = {__builtin_copysignf(0.5f, v[i].x), __builtin_copysignf(0.5f, v[i].y)};
+        const v2f t = __builtin_elementwise_fma(v[i], rcb2, hs);
         c[2 * i] = med3_i32(cvt_i32_sat(t.x), lo, hi);
         c[2 * i + 1] = med3_i32(cvt_i32_sat(t.y), lo, hi);
     }
@@ -155,7 +140,7 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
 }
 
 // ---- producer arithmetic, 8 fp16 values per call: fq_producers.hip's kernels and the decode
-// kernel's fused prologues (fq_gemm.hip, PRO = 1 / 2) share these, so the two give the same bits.
+// kernel's fused prologues (fq_gemm.hip, PRO = 1 / 2 / 4) share these, so the two give the same bits.
 // half_clamp = clamp_inf_for_half (reduce_kernel_utils.cuh:357-361): clamp to +-(65504 - 1000).
 __device__ __forceinline__ float half_clamp_f(float v) {
     return v > 0.0f ? fminf(v, 65504.0f - 1000.0f) : fmaxf(v, -65504.0f + 1000.0f);
@@ -219,6 +204,78 @@ __device__ __forceinline__ uint4 silu_mul8(uint4 g4, uint4 u4) {
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// ---- OPT-family LayerNorm producer arithmetic (generalAddBiasResidualLayerNormOpt2FlexQFusion,
+// e2e .../kernels/layernorm_kernels.cu:316-575), 8 fp16 values per call:
+//   v      = ((0 + float(bias)) + float(residual)) + float(input)   in fp32, absent terms skipped (:357-385)
+//   h      = half(v)                                                 (the residual output, :393-395)
+//   sums   s += v[2i] + v[2i+1],  q += v[2i] * v[2i] + v[2i+1] * v[2i+1]   per half2 pair (:396-397)
+//   mean   = (s / (K/2)) / 2,  rs = 1 / sqrt(((q / (K/2)) / 2 - mean * mean) + eps)   (:403-404; IEEE
+//            where the reference has rsqrtf)
+//   normed = ((h - half(mean)) * half(rs)) * gamma [+ beta]   every step an fp16 operation (:412-416)
+// The reference's fp32 sums follow its launch shape; this build's order (per thread over its chunks,
+// the pairs of a chunk in order, wave_sum64, the waves in order) is the one the oracle restates.
+__device__ __forceinline__ void ln_add8(const uint4 *in, const uint4 &res, const uint4 *bias, float (&v)[8]) {
+#pragma clang fp contract(off)
+    const uint32_t r[4] = {res.x, res.y, res.z, res.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float a0 = 0.0f, a1 = 0.0f;
+        if (bias) {
+            const uint32_t b[4] = {bias->x, bias->y, bias->z, bias->w};
+            a0 = a0 + lo_f(b[i]);
+            a1 = a1 + hi_f(b[i]);
+        }
+        a0 = a0 + lo_f(r[i]);
+        a1 = a1 + hi_f(r[i]);
+        if (in) {
+            const uint32_t x[4] = {in->x, in->y, in->z, in->w};
+            a0 = a0 + lo_f(x[i]);
+            a1 = a1 + hi_f(x[i]);
+        }
+        v[2 * i] = a0;
+        v[2 * i + 1] = a1;
+    }
+}
+__device__ __forceinline__ uint4 ln_pack8(const float (&v)[8]) {
+    return make_uint4(pack_h2(v[0], v[1]), pack_h2(v[2], v[3]), pack_h2(v[4], v[5]), pack_h2(v[6], v[7]));
+}
+__device__ __forceinline__ void ln_sums8(const float (&v)[8], float &s, float &q) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        s = s + (v[2 * i] + v[2 * i + 1]);
+        q = q + (__fmul_rn(v[2 * i], v[2 * i]) + __fmul_rn(v[2 * i + 1], v[2 * i + 1]));
+    }
+}
+// (mean, 1 / sqrt(var + eps)) from the row sums; K = the row length
+__device__ __forceinline__ float2 ln_stats(float s, float q, int K, float eps) {
+#pragma clang fp contract(off)
+    const float n = (float)(K / 2);
+    const float mean = (s / n) / 2.0f;
+    const float var = ((q / n) / 2.0f - __fmul_rn(mean, mean)) + eps;
+    return make_float2(mean, 1.0f / __builtin_sqrtf(var));
+}
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+// normed = ((h - mean_h) * rs_h) * gamma [+ beta], packed fp16 (v_pk_sub/mul/add_f16, round to nearest)
+__device__ __forceinline__ uint4 ln_apply8(uint4 h, float2 st, uint4 gamma, const uint4 *beta) {
+#pragma clang fp contract(off)
+    const _Float16 mh = (_Float16)st.x, rh = (_Float16)st.y;
+    const h2v m2 = {mh, mh}, r2 = {rh, rh};
+    const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, gw[4] = {gamma.x, gamma.y, gamma.z, gamma.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        h2v a = __builtin_bit_cast(h2v, hw[i]);
+        a = ((a - m2) * r2) * __builtin_bit_cast(h2v, gw[i]);
+        if (beta) {
+            const uint32_t bw[4] = {beta->x, beta->y, beta->z, beta->w};
+            a = a + __builtin_bit_cast(h2v, bw[i]);
+        }
+        o[i] = __builtin_bit_cast(uint32_t, a);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // Sum of a float over the 64 lanes of a wave, in a fixed tree: lane pairs, quads, 8- and 16-lane
 // halves on DPP (after each step every lane of a block holds the block's sum, so a mirror partner
 // is as good as the xor partner), then the four 16-lane rows as (r0 + r1) + (r2 + r3).  The same
@@ -238,11 +295,13 @@ __device__ __forceinline__ float wave_sum64(float v) {
 
 // arguments of a producer fused into the decode linear's prologue (fq_gemm.hip, PRO = 1 / 2)
 struct DecodePro {
-    const uint16_t *in;     // PRO 1: added to the residual (or null); PRO 2: up
-    const uint16_t *gamma;  // PRO 1
-    uint16_t *res_out;      // PRO 1 with `in`: residual + in (never the residual itself)
-    float eps;              // PRO 1
+    const uint16_t *in;     // PRO 1 / 4: added to the residual (or null); PRO 2: up
+    const uint16_t *gamma;  // PRO 1 / 4
+    uint16_t *res_out;      // PRO 1 with `in`, PRO 4: residual + in (never the residual itself)
+    float eps;              // PRO 1 / 4
     int ldh;                // row stride (elements) of xh and `in` (PRO 2; K otherwise)
+    const uint16_t *beta;   // PRO 4 (or null)
+    const uint16_t *bias;   // PRO 4 (or null)
 };
 
 // ---- fq6 weight unpack ----------------------------------------------------------------------

@@ -93,6 +93,9 @@ __host__ __device__ inline int decode_xwin_bytes(int ng, int M, int xwin) { retu
 // per-wave LDS: [ring D x SLOT][ws: nb x 8 dwords][xs: ng x XSR dwords][x: ng x M x 128 B]
 //               [FUSE: fp16 window]
 // (wm windows side by side: 3 for the RMSNorm prologue -- residual, input, gamma --, 2 for SiLU * up)
+// fp16 windows a fused producer's prologue fetches: RMSNorm 3 (residual, input, gamma), SiLU 2 (gate,
+// up), LayerNorm 5 (residual, input, gamma, beta, bias)
+__host__ __device__ constexpr int decode_pro_windows(int pro) { return pro == 1 ? 3 : pro == 2 ? 2 : pro == 4 ? 5 : 1; }
 __host__ __device__ inline int decode_wave_lds(int MT, int XS, int SS, int ng, int nb, int M, int xwin, int wm = 1) {
     const int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;
     int b = decode_depth_for(MT, XS, decode_slot(MT, XS, SS), 2 + XP + (SS ? 2 : 0)) * decode_slot(MT, XS, SS);
@@ -226,6 +229,26 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
 #define FQ_PRO_ABL 0
 #endif
 
+// The decode stream loop's V2 form (buffer-resource weight DMA with scalar block offsets, refill
+// right after the slot's plane reads, dequant lagged one block); 0 = the round-3 loop (A/B builds)
+#ifndef FQ_DEC_V2
+#define FQ_DEC_V2 1
+#endif
+
+// Dequantize one block's MFMA accumulators (the reference's epilogue order,
+// flexq_bmma_kernel.h:359-373): c[r] += float(acc[r]) * float(half(xs * ws)).
+template <int ABL>
+__device__ __forceinline__ void dequant4(float (&c)[4], v4i acc, __half2 p01, __half2 p23) {
+    if (ABL & 1024) {  // (development: no dequant, accumulators kept alive)
+        c[0] = __int_as_float(__float_as_int(c[0]) ^ acc[0] ^ acc[1] ^ acc[2] ^ acc[3]);
+        return;
+    }
+    c[0] = fmaf((float)acc[0], __low2float(p01), c[0]);
+    c[1] = fmaf((float)acc[1], __high2float(p01), c[1]);
+    c[2] = fmaf((float)acc[2], __low2float(p23), c[2]);
+    c[3] = fmaf((float)acc[3], __high2float(p23), c[3]);
+}
+
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
@@ -287,7 +310,7 @@ __device__ __forceinline__ void decode_body(
     // blocked w-scales of the image: fp16 [NT][G][16] after the weight blocks (fq_quant.hip)
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
 
-    const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, FUSE ? xwin : 0, PRO == 1 ? 3 : PRO == 2 ? 2 : 1);
+    const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, FUSE ? xwin : 0, decode_pro_windows(PRO));
     char *ring = smem + wid * wl;
     char *ws_st = ring + D * C::SLOT;                                 // staged w-scales
     char *xs_st = ws_st + (SS ? 0 : decode_wsst_bytes(ngmax * IPW));  // staged x-scales
@@ -295,7 +318,7 @@ __device__ __forceinline__ void decode_body(
     const int EM = M * 16;                                            // live elements of a tile
     float *red = reinterpret_cast<float *>(smem + NW * wl);           // [RC][NW][M*16]
     int *flag = reinterpret_cast<int *>(red + RC * NW * EM);          // [IPW]
-    char *wsum = reinterpret_cast<char *>(flag) + ((4 * IPW + 15) & ~15);  // PRO 1: [NW] floats
+    char *wsum = reinterpret_cast<char *>(flag) + ((4 * IPW + 15) & ~15);  // PRO 1: [NW], PRO 4: [2][NW] floats
 
     auto item_tile = [&](int it) { return t0 + it * tstep; };
 
@@ -346,6 +369,12 @@ __device__ __forceinline__ void decode_body(
                 __builtin_amdgcn_global_load_lds(pro.gamma + off, LDS_PTR(xh_st + 2 * xwb + c * 256), 16, 0, 0);
             if (PRO == 2 && !(FQ_PRO_ABL & 8))
                 __builtin_amdgcn_global_load_lds(pro.in + row * ldh + off, LDS_PTR(xh_st + xwb + c * 256), 16, 0, 0);
+            if (PRO == 4) {  // (M = 1: the residual row is xh; gamma, beta, bias are per column)
+                if (pro.in) __builtin_amdgcn_global_load_lds(pro.in + off, LDS_PTR(xh_st + xwb + c * 256), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(pro.gamma + off, LDS_PTR(xh_st + 2 * xwb + c * 256), 16, 0, 0);
+                if (pro.beta) __builtin_amdgcn_global_load_lds(pro.beta + off, LDS_PTR(xh_st + 3 * xwb + c * 256), 16, 0, 0);
+                if (pro.bias) __builtin_amdgcn_global_load_lds(pro.bias + off, LDS_PTR(xh_st + 4 * xwb + c * 256), 16, 0, 0);
+            }
         }
     };
     auto x_store = [&](int rg, uint2 codes, uint16_t sh) {
@@ -458,10 +487,25 @@ __device__ __forceinline__ void decode_body(
     };
 
     // ---- the ring over the wave's block sequence
+    // V2 (fully staged variants): the weight DMAs address the image through a buffer resource with
+    // the block's byte offset in an SGPR (advanced incrementally: +1 block per group, a jump per
+    // item), so a refill is two buffer_load ... lds instructions with no per-lane 64-bit address
+    // math on the path from "slot landed" to "slot refilled" (the host keeps the image < 4 GiB).
+    constexpr bool V2 = FQ_DEC_V2 && XS == 0 && SS == 0;
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, (int)((uint32_t)NT * G * FQ_BLOCK), 0x00020000);
+    const uint32_t wvo = lane * 16;
+    uint32_t roff = ((uint32_t)t0 * G + ga) * FQ_BLOCK;                 // next block to issue (V2)
+    const uint32_t rjump = ((uint32_t)tstep * G - ng + 1) * FQ_BLOCK;  // an item's last group -> the next item's first
     const char *wbytes = reinterpret_cast<const char *>(wpk) + lane * 16;
     auto issue = [&](int it, int j, int slot) {  // block (item it, group ga + j) -> slot
         const int t = item_tile(it), g = ga + j;
         char *dst = ring + slot * C::SLOT;
+        if constexpr (V2) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst), 16, wvo, roff, 0, FQ_W_AUX);
+            if (lane < 32) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + 1024), 16, wvo, roff + 1024, 0, FQ_W_AUX);
+            return;
+        }
         const char *src = wbytes + ((long)t * G + g) * FQ_BLOCK;
         __builtin_amdgcn_global_load_lds(src, LDS_PTR(dst), 16, 0, FQ_W_AUX);
         if (lane < 32) __builtin_amdgcn_global_load_lds(src + 1024, LDS_PTR(dst + 1024), 16, 0, FQ_W_AUX);
@@ -486,14 +530,20 @@ __device__ __forceinline__ void decode_body(
     // first-needed ones go first.
     if (FUSE && n > 0) x_fetch(0);
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
+    auto advance = [&]() {
+        if (++rj == ng) {
+            rj = 0;
+            ++rit;
+            roff += rjump;
+        } else {
+            roff += FQ_BLOCK;
+        }
+    };
     if (n > 0) {
 #pragma unroll
         for (int i = 0; i < D; i++) {
             issue(rit, rj, i);
-            if (i + 1 < n && ++rj == ng) {  // (a short sequence re-issues its last block)
-                rj = 0;
-                ++rit;
-            }
+            if (i + 1 < n) advance();  // (a short sequence re-issues its last block)
             if (i == 0) stage_all();
         }
     }
@@ -527,9 +577,44 @@ __device__ __forceinline__ void decode_body(
             const uint16_t sh = quant_group16(rms_apply8(r, make_uint4(gg[0], gg[1], gg[2], gg[3]), rms_scale(ss, K, pro.eps)),
                                               abits, codes);
             x_store(lane >> 4, codes, sh);
+        } else if (PRO == 4) {  // bias + residual + input, LayerNorm (lane = chunk 64 wid + lane, as PRO 1)
+            const uint32_t xb = lds_addr(xh_st) + lane * 16;
+            v4i rr = ds_read_b128(xb), ii = ds_read_b128(xb + xwb), gg = ds_read_b128(xb + 2 * xwb);
+            v4i be = ds_read_b128(xb + 3 * xwb), bi = ds_read_b128(xb + 4 * xwb);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rr), "+v"(ii), "+v"(gg), "+v"(be), "+v"(bi)::"memory");
+            const uint4 in4 = make_uint4(ii[0], ii[1], ii[2], ii[3]), bi4 = make_uint4(bi[0], bi[1], bi[2], bi[3]);
+            const uint4 be4 = make_uint4(be[0], be[1], be[2], be[3]);
+            float v[8];
+            ln_add8(pro.in ? &in4 : nullptr, make_uint4(rr[0], rr[1], rr[2], rr[3]), pro.bias ? &bi4 : nullptr, v);
+            const uint4 h = ln_pack8(v);
+            if (blockIdx.x == 0 && pro.res_out) *reinterpret_cast<uint4 *>(pro.res_out + 8 * (64 * wid + lane)) = h;
+            float s = 0.0f, q = 0.0f;
+            ln_sums8(v, s, q);
+            s = wave_sum64(s);
+            q = wave_sum64(q);
+            if (lane == 0) {
+                ds_write_b32(lds_addr(wsum) + 4 * wid, __float_as_uint(s));
+                ds_write_b32(lds_addr(wsum) + 4 * (NW + wid), __float_as_uint(q));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            v4i s0 = ds_read_b128(lds_addr(wsum)), s1 = ds_read_b128(lds_addr(wsum) + 16);
+            v4i q0 = ds_read_b128(lds_addr(wsum) + 4 * NW), q1 = ds_read_b128(lds_addr(wsum) + 4 * NW + 16);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s0), "+v"(s1), "+v"(q0), "+v"(q1)::"memory");
+            float S = __int_as_float(s0[0]), Q = __int_as_float(q0[0]);
+#pragma unroll
+            for (int w = 1; w < NW; w++) {
+                S = S + __int_as_float(w < 4 ? s0[w] : s1[w - 4]);
+                Q = Q + __int_as_float(w < 4 ? q0[w] : q1[w - 4]);
+            }
+            uint2 codes;
+            const uint16_t sh = quant_group16(ln_apply8(h, ln_stats(S, Q, K, pro.eps), make_uint4(gg[0], gg[1], gg[2], gg[3]),
+                                                        pro.beta ? &be4 : nullptr),
+                                              abits, codes);
+            x_store(lane >> 4, codes, sh);
         } else if (PRO == 3) {
             x_unpack(0);
-        } else {
+        } else if (!(ABL & 2048)) {  // (development 2048: no quantizer, codes left undefined)
             x_quant(0);
         }
         FQ_STAMP(6);
@@ -552,7 +637,8 @@ __device__ __forceinline__ void decode_body(
 #pragma unroll
     for (int rg = 0; rg < RG; rg++) arow[rg] = 16 * rg + (lane & 15) < M ? 16 * rg + (lane & 15) : M - 1;
     const int Npad = NT * 16;
-    int i = 0;  // position in the wave's block sequence
+    int i = 0;     // position in the wave's block sequence
+    int rslot = 0;  // its ring slot (V2: counted, no i % D)
     for (int it = 0; it < nit; it++) {
         const int t = item_tile(it);
         const int col = 16 * t + (lane & 15);
@@ -561,15 +647,23 @@ __device__ __forceinline__ void decode_body(
         for (int rg = 0; rg < RG; rg++)
 #pragma unroll
             for (int r = 0; r < 4; r++) cur[rg][r] = 0.f;
+        // V2: block j's dequant runs after block j + 1's MFMAs are issued (same item), so the wave
+        // does not stall on the MFMA result between a refill and the next ring wait
+        v4i pacc[RG];
+        __half2 pp01[RG], pp23[RG];
         for (int j = 0; j < ng; j++, i++) {
-            const int g = ga + j, slot = i % D;
-            const int later = (n - 1 - i) < (D - 1) ? (n - 1 - i) : (D - 1);
-            wait_ring<C::U, D>(later);  // this slot (and every older DMA, the staging included) landed
+            const int g = ga + j, slot = V2 ? rslot : i % D;
+            if (V2 && i + D <= n) {
+                wait_ring_steady<C::U, D>();  // D - 1 younger blocks in flight: the common case
+            } else {
+                const int later = (n - 1 - i) < (D - 1) ? (n - 1 - i) : (D - 1);
+                wait_ring<C::U, D>(later);  // this slot (and every older DMA, the staging included) landed
+            }
             if (i == 0) FQ_STAMP(2);
             const uint32_t sp = lds_addr(ring + slot * C::SLOT);
-            const v2u p0 = ds_read_b64(sp + lane * 8);
-            const v2u p1 = ds_read_b64(sp + 512 + lane * 8);
-            const v2u p2 = ds_read_b64(sp + 1024 + lane * 8);
+            v2u p0 = ds_read_b64(sp + lane * 8);
+            v2u p1 = ds_read_b64(sp + 512 + lane * 8);
+            v2u p2 = ds_read_b64(sp + 1024 + lane * 8);
             v4i a[RG][2];
 #pragma unroll
             for (int rg = 0; rg < RG; rg++) {
@@ -579,19 +673,33 @@ __device__ __forceinline__ void decode_body(
                 for (int s = 0; s < 2; s++) a[rg][s] = ds_read_b128(xrow + xswz(arow[rg], 4 * s + (lane >> 4)));
             }
             const uint32_t wsa = (SS ? sp + C::WS_OFF : lds_addr(ws_st) + i * 32) + 2 * (lane & 15);
-            const uint32_t wsv = ds_read_u16(wsa);
+            uint32_t wsv = ds_read_u16(wsa);
             v4i xd[RG];  // x-scales of rows 16rg + 4(lane>>4) .. +3, one per dword
             const uint32_t xsa = SS ? sp + C::XS_OFF : lds_addr(xs_st + j * XSR * 4);
 #pragma unroll
             for (int rg = 0; rg < RG; rg++) xd[rg] = ds_read_b128(xsa + 4 * (16 * rg + 4 * (lane >> 4)));
-            // every read has landed, and the slot's bytes are in registers before its refill
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (i + D < n) {  // refill: block i + D
-                issue(rit, rj, slot);
-                if (++rj == ng) {
-                    rj = 0;
-                    ++rit;
+            if constexpr (V2) {
+                // LDS reads return in order: once the three plane reads (the only bytes read from
+                // the slot; activations and scales are staged elsewhere) have landed, refill the
+                // slot, then wait for the rest
+                asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(p0), "+v"(p1), "+v"(p2) : "i"(3 * RG + 1) : "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + D < n) {  // refill: block i + D
+                    issue(rit, rj, slot);
+                    advance();
+                }
+                rslot = rslot + 1 == D ? 0 : rslot + 1;
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wsv)::"memory");
+#pragma unroll
+                for (int rg = 0; rg < RG; rg++) asm volatile("" : "+v"(a[rg][0]), "+v"(a[rg][1]), "+v"(xd[rg]));
+                __builtin_amdgcn_sched_barrier(0);
+            } else {
+                // every read has landed, and the slot's bytes are in registers before its refill
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                if (i + D < n) {  // refill: block i + D
+                    issue(rit, rj, slot);
+                    advance();
                 }
             }
 
@@ -599,20 +707,36 @@ __device__ __forceinline__ void decode_body(
                 cur[0][0] += (float)(p0[0] ^ p1[1] ^ p2[0] ^ a[0][1][0]) + (float)wsv + (float)xd[0][0];
                 continue;
             }
-            const v4i b0 = unpack_fq6(p0[0], p1[0], p2[0]), b1 = unpack_fq6(p0[1], p1[1], p2[1]);
+            v4i b0, b1;
+            if (ABL & 256) {  // (development: no unpack -- the raw plane words as operands)
+                b0 = v4i{(int)p0[0], (int)p1[0], (int)p2[0], (int)p0[1]};
+                b1 = v4i{(int)p1[1], (int)p2[1], (int)p0[0], (int)p1[0]};
+            } else {
+                b0 = unpack_fq6(p0[0], p1[0], p2[0]);
+                b1 = unpack_fq6(p0[1], p1[1], p2[1]);
+            }
             const __half2 w2 = __half2half2(__ushort_as_half((uint16_t)wsv));
 #pragma unroll
             for (int rg = 0; rg < RG; rg++) {
-                v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][0], b0, v4i{0, 0, 0, 0}, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][1], b1, acc, 0, 0, 0);
+                v4i acc;
+                if (ABL & 512) {  // (development: no MFMA)
+                    acc = v4i{a[rg][0][0] ^ b0[0], a[rg][0][1] ^ b0[1], a[rg][1][2] ^ b1[2], a[rg][1][3] ^ b1[3]};
+                } else {
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][0], b0, v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[rg][1], b1, acc, 0, 0, 0);
+                }
                 const uint32_t x01 = __builtin_amdgcn_perm((uint32_t)xd[rg][1], (uint32_t)xd[rg][0], 0x05040100u);
                 const uint32_t x23 = __builtin_amdgcn_perm((uint32_t)xd[rg][3], (uint32_t)xd[rg][2], 0x05040100u);
                 const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&x01), w2);  // fp16-rounded
                 const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&x23), w2);  // scale product
-                cur[rg][0] = fmaf((float)acc[0], __low2float(p01), cur[rg][0]);
-                cur[rg][1] = fmaf((float)acc[1], __high2float(p01), cur[rg][1]);
-                cur[rg][2] = fmaf((float)acc[2], __low2float(p23), cur[rg][2]);
-                cur[rg][3] = fmaf((float)acc[3], __high2float(p23), cur[rg][3]);
+                if (V2) {
+                    if (j > 0) dequant4<ABL>(cur[rg], pacc[rg], pp01[rg], pp23[rg]);
+                    pacc[rg] = acc;
+                    pp01[rg] = p01;
+                    pp23[rg] = p23;
+                } else {
+                    dequant4<ABL>(cur[rg], acc, p01, p23);
+                }
                 if (DBG) {
 #pragma unroll
                     for (int r = 0; r < 4; r++) {
@@ -621,6 +745,10 @@ __device__ __forceinline__ void decode_body(
                     }
                 }
             }
+        }
+        if (V2 && ng > 0 && !(ABL & 2)) {  // the item's last block
+#pragma unroll
+            for (int rg = 0; rg < RG; rg++) dequant4<ABL>(cur[rg], pacc[rg], pp01[rg], pp23[rg]);
         }
 
         // ---- item end: the wave's partial tile goes to reduction slot it % RC; every RC items
@@ -763,8 +891,26 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_pro_kern
     const int K = (w1 & 0x1fff) * FQ_GROUP, S = (w1 >> 13) & 1023;
     const int IPW = w2 & 0xffff, RC = w2 >> 16;
     const int Mall = w3 & 1023, ir = (w3 >> 10) & 2047, grid = w3 >> 21;
-    const DecodePro pro = {pin, gamma, res_out, eps, ldh};
+    const DecodePro pro = {pin, gamma, res_out, eps, ldh, nullptr, nullptr};
     decode_body<MT, 0, 0, true, false, 0, false, PRO, false>(
+        nullptr, nullptr, xh, abits, wpk, Mall, N, K, d, nullptr, reinterpret_cast<float *>(ws + FQ_TICKET_BYTES),
+        reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, IPW - (ir != 0), ir, 1, nullptr, pro, grid);
+}
+
+// The fused LayerNorm producer's kernel (PRO 4, M = 1): the pro kernel's list with beta and bias
+// after the packed fields.
+template <int MT>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ln_kernel(
+    const uint16_t *__restrict__ xh, const uint32_t *__restrict__ wpk, const uint16_t *__restrict__ pin,
+    const uint16_t *__restrict__ gamma, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+    const uint16_t *__restrict__ beta, const uint16_t *__restrict__ bias, float eps, uint16_t *__restrict__ d,
+    char *__restrict__ ws, uint16_t *__restrict__ res_out) {
+    const int N = w0 & 0x1fffff, abits = (w0 >> 21) & 15, xwin = w0 >> 25;
+    const int K = (w1 & 0x1fff) * FQ_GROUP, S = (w1 >> 13) & 1023;
+    const int IPW = w2 & 0xffff, RC = w2 >> 16;
+    const int Mall = w3 & 1023, ir = (w3 >> 10) & 2047, grid = w3 >> 21;
+    const DecodePro pro = {pin, gamma, res_out, eps, K, beta, bias};
+    decode_body<MT, 0, 0, true, false, 0, false, 4, false>(
         nullptr, nullptr, xh, abits, wpk, Mall, N, K, d, nullptr, reinterpret_cast<float *>(ws + FQ_TICKET_BYTES),
         reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, IPW - (ir != 0), ir, 1, nullptr, pro, grid);
 }
@@ -1462,9 +1608,9 @@ static size_t decode_lds_bytes(const DecodePlan &p, int M, int N, int K) {
     const int NW = decode_waves(p.MT);
     const int Gz = (K / FQ_GROUP + p.S - 1) / p.S;
     const int ngmax = (Gz + NW - 1) / NW;
-    const int wm = p.pro == 1 ? 3 : p.pro == 2 ? 2 : 1;
+    const int wm = decode_pro_windows(p.pro);
     return (size_t)NW * decode_wave_lds(p.MT, p.XS, p.SS, ngmax, ngmax * p.IPW, M, p.xwin, wm) +
-           (size_t)p.RC * NW * M * 16 * 4 + ((4 * (size_t)p.IPW + 15) & ~(size_t)15) + 4 * NW + 16;
+           (size_t)p.RC * NW * M * 16 * 4 + ((4 * (size_t)p.IPW + 15) & ~(size_t)15) + 8 * NW + 16;
 }
 
 // Cost model, in quarter-blocks of one wave's stream (one 1.5 KiB block per wave at the
@@ -1681,6 +1827,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
     float *slabs = p.S > 1 ? (float *)((char *)a.workspace + kTicketBytes) : nullptr;
     const size_t lds = decode_lds_bytes(p, a.M, a.N, a.K);
     const dim3 grid(p.grid), block(decode_waves(MT) * 64);
+    if ((size_t)p.NT * (a.K / FQ_GROUP) * FQ_BLOCK >= ((size_t)1 << 32)) return FQ_ERR_SHAPE;  // (buffer offsets)
     DecodePacked pk;
     const int gw = p.grid / p.NCH, items = p.NT * p.S;
     if (items / gw != p.IPW - (items % gw != 0) ||
@@ -1698,9 +1845,18 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         return FQ_OK;                                                                                         \
     }
         FQ_ABL(2) FQ_ABL(4) FQ_ABL(6) FQ_ABL(8) FQ_ABL(14) FQ_ABL(16) FQ_ABL(48) FQ_ABL(112)
+        FQ_ABL(256) FQ_ABL(512) FQ_ABL(1024) FQ_ABL(768) FQ_ABL(1536) FQ_ABL(1792) FQ_ABL(2048) FQ_ABL(2052)
 #undef FQ_ABL
     }
 #endif
+    if constexpr (PRO == 4) {  // the fused LayerNorm (M = 1, S = 1)
+        if (p.NCH != 1) return FQ_ERR_SHAPE;
+        hipLaunchKernelGGL((fq_gemm_decode_ln_kernel<MT>), grid, block, lds, stream, a.xh, (const uint32_t *)a.wpk,
+                           a.pro.in, a.pro.gamma, pk.w0, pk.w1, pk.w2, pk.w3, a.pro.beta, a.pro.bias, a.pro.eps, a.d,
+                           (char *)a.workspace, a.pro.res_out);
+        FQ_LAUNCH_CHECK();
+        return FQ_OK;
+    }
     if constexpr (PRO != 0) {  // the fused producers (FUSE, S as planned, no debug output, no gather)
         if (p.NCH != 1) return FQ_ERR_SHAPE;  // (the producer plans have one row chunk)
         hipLaunchKernelGGL((fq_gemm_decode_pro_kernel<MT, PRO>), grid, block, lds, stream, a.xh,
@@ -1795,7 +1951,12 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
 // kernel and the GEMM instead.
 static bool pro_fuse(int pro, int M, int N, int K, DecodePlan *p) {
     if (!decode_fuse(M, N, K, p, pro)) return false;
-    return pro != 1 || (M == 1 && p->MT == 4 && p->S == 1 && K == 4 * FQ_GROUP * decode_waves(4));
+    return (pro != 1 && pro != 4) || (M == 1 && p->MT == 4 && p->S == 1 && K == 4 * FQ_GROUP * decode_waves(4));
+}
+extern "C" size_t fq_layernorm_linear_scratch_bytes(int M, int N, int K) {
+    DecodePlan p;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || pro_fuse(4, M, N, K, &p)) return 0;
+    return (size_t)M * K + (size_t)M * (K / FQ_GROUP) * 2;
 }
 extern "C" size_t fq_rmsnorm_linear_scratch_bytes(int M, int N, int K) {
     DecodePlan p;
@@ -1812,7 +1973,7 @@ fq_status fq_decode_linear_pro(int pro, const uint16_t *xh, const DecodePro &pro
                                const void *w_packed, uint16_t *d, void *workspace, size_t workspace_bytes,
                                hipStream_t s, bool *launched) {
     *launched = false;
-    if (pro != 1 && pro != 2) return FQ_ERR_SHAPE;
+    if (pro != 1 && pro != 2 && pro != 4) return FQ_ERR_SHAPE;
     DecodePlan p;
     if (!pro_fuse(pro, M, N, K, &p)) return FQ_OK;
     const size_t need = fq_gemm_workspace_bytes(M, N, K);
@@ -1820,6 +1981,7 @@ fq_status fq_decode_linear_pro(int pro, const uint16_t *xh, const DecodePro &pro
     DecodeArgs a = {nullptr, nullptr, xh, abits, w_packed, M, N, K, d, nullptr, workspace, nullptr, prod};
     *launched = true;
     if (pro == 1) return launch_decode<4, 0, 0, true, false, false, 1>(p, a, s);
+    if (pro == 4) return launch_decode<4, 0, 0, true, false, false, 4>(p, a, s);
     switch (p.MT) {
         case 4: return launch_decode<4, 0, 0, true, false, false, 2>(p, a, s);
         case 8: return launch_decode<8, 0, 0, true, false, false, 2>(p, a, s);

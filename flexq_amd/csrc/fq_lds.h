@@ -90,6 +90,12 @@ __device__ __forceinline__ void wait_ring(int later) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// the ring's steady state: D - 1 younger blocks of U DMA instructions stay in flight
+template <int U, int D>
+__device__ __forceinline__ void wait_ring_steady() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((D - 1) * U) : "memory");
+}
+
 // Activation rows in LDS are 128 B (one group) with their eight 16-byte chunks XOR-swizzled by
 // (row & 7): the A-operand read (16 rows x 16 B per k-chunk) is then conflict-free per 8 lanes.
 __host__ __device__ inline int xswz(int row, int chunk) { return (chunk ^ (row & 7)) * 16; }

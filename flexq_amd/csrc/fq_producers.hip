@@ -165,3 +165,111 @@ extern "C" fq_status fq_silu_mul_quantize(const uint16_t *gate, const uint16_t *
     FQ_LAUNCH_CHECK();
     return FQ_OK;
 }
+
+// ---- OPT-family LayerNorm producer: residual [+ input] [+ bias] -> LayerNorm (gamma, beta) -> codes.
+// generalAddBiasResidualLayerNormOpt2FlexQFusion (e2e .../kernels/layernorm_kernels.cu:316-575; the
+// pre-attention form invokeGeneralLayerNorm :2325-2420 is residual only, no bias, no input).  The
+// reference normalises in block y = 0 and quantizes in every block of the row after a block-local
+// barrier (the cross-block race of SURVEY.md §5); here one workgroup owns the row, as for RMSNorm.
+// Arithmetic: fq_common.h ln_add8 .. ln_apply8 (restated by oracle/fq_oracle.c fqo_layernorm_quantize).
+template <int T>
+__global__ __launch_bounds__(T) void fq_layernorm_quant_kernel(const uint16_t *__restrict__ input,
+                                                               const uint16_t *residual,
+                                                               const uint16_t *__restrict__ bias, uint16_t *res_out,
+                                                               const uint16_t *__restrict__ gamma,
+                                                               const uint16_t *__restrict__ beta, float eps, int M,
+                                                               int K, int abits, int8_t *__restrict__ xq,
+                                                               uint16_t *__restrict__ xs,
+                                                               uint16_t *__restrict__ normed) {
+    constexpr int MAXCH = PR_KMAX / 8 / T;
+    __shared__ float wsum[2 * (T / 64)];
+    const int m = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int nq = K / 8;
+    const size_t row = (size_t)m * K;
+    uint4 h[MAXCH];
+    float s = 0.0f, q = 0.0f;
+#pragma unroll
+    for (int c = 0; c < MAXCH; c++) {
+        const int qi = c * T + t;
+        h[c] = make_uint4(0, 0, 0, 0);
+        if (c * T < nq && qi < nq) {
+            const uint4 res = *reinterpret_cast<const uint4 *>(residual + row + 8 * (size_t)qi);
+            uint4 in, bv;
+            if (input) in = *reinterpret_cast<const uint4 *>(input + row + 8 * (size_t)qi);
+            if (bias) bv = *reinterpret_cast<const uint4 *>(bias + 8 * (size_t)qi);
+            float v[8];
+            ln_add8(input ? &in : nullptr, res, bias ? &bv : nullptr, v);
+            h[c] = ln_pack8(v);
+            // (res_out may be the residual itself: each thread owns its chunks)
+            if (res_out) *reinterpret_cast<uint4 *>(res_out + row + 8 * (size_t)qi) = h[c];
+            ln_sums8(v, s, q);
+        }
+    }
+    s = wave_sum64(s);
+    q = wave_sum64(q);
+    if (lane == 0) {
+        wsum[wid] = s;
+        wsum[T / 64 + wid] = q;
+    }
+    __syncthreads();
+    float S = wsum[0], Q = wsum[T / 64];
+#pragma unroll
+    for (int w = 1; w < T / 64; w++) {
+        S = S + wsum[w];
+        Q = Q + wsum[T / 64 + w];
+    }
+    const float2 st = ln_stats(S, Q, K, eps);
+#pragma unroll
+    for (int c = 0; c < MAXCH; c++) {
+        if (c * T >= nq) break;  // block-uniform
+        const int qi = c * T + t;
+        const bool valid = qi < nq;  // whole 16-lane groups (nq % 16 == 0)
+        uint4 nv = make_uint4(0, 0, 0, 0);
+        if (valid) {
+            const uint4 g = *reinterpret_cast<const uint4 *>(gamma + 8 * (size_t)qi);
+            uint4 b;
+            if (beta) b = *reinterpret_cast<const uint4 *>(beta + 8 * (size_t)qi);
+            nv = ln_apply8(h[c], st, g, beta ? &b : nullptr);
+            if (normed) *reinterpret_cast<uint4 *>(normed + row + 8 * (size_t)qi) = nv;
+        }
+        quant_store(nv, abits, valid, xq + row + 8 * (size_t)qi, xs + (size_t)(qi >> 4) * M + m, (t & 15) == 0);
+    }
+}
+
+static bool overlaps(const void *a, size_t na, const void *b, size_t nb) {
+    if (!a || !b) return false;
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return x < y + nb && y < x + na;
+}
+
+extern "C" fq_status fq_layernorm_quantize(const uint16_t *input, const uint16_t *residual, const uint16_t *bias,
+                                           uint16_t *res_out, const uint16_t *gamma, const uint16_t *beta, float eps,
+                                           int M, int K, int abits, int8_t *xq, uint16_t *xs, uint16_t *normed_out,
+                                           fq_stream_t stream) {
+    if (!residual || !gamma || !xq || !xs) return FQ_ERR_NULL;
+    if (M <= 0 || K <= 0 || K % FQ_GROUP || K > PR_KMAX) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    if (!aligned16(residual) || !aligned16(gamma) || !aligned16(xq) || (input && !aligned16(input)) ||
+        (bias && !aligned16(bias)) || (beta && !aligned16(beta)) || (res_out && !aligned16(res_out)) ||
+        (normed_out && !aligned16(normed_out)))
+        return FQ_ERR_SHAPE;
+    // res_out may be the residual (in place) but must not overlap the input, bias, gamma or beta
+    const size_t rb = (size_t)M * K * 2, vb = (size_t)K * 2;
+    if (res_out && (overlaps(res_out, rb, input, rb) || overlaps(res_out, rb, bias, vb) ||
+                    overlaps(res_out, rb, gamma, vb) || overlaps(res_out, rb, beta, vb) ||
+                    (res_out != residual && overlaps(res_out, rb, residual, rb))))
+        return FQ_ERR_SHAPE;
+    const int nq = K / 8;
+#define FQ_LN_LAUNCH(T)                                                                                             \
+    hipLaunchKernelGGL(fq_layernorm_quant_kernel<T>, dim3(M), dim3(T), 0, (hipStream_t)stream, input, residual,  \
+                       bias, res_out, gamma, beta, eps, M, K, abits, xq, xs, normed_out)
+    if (nq <= 256)
+        FQ_LN_LAUNCH(256);
+    else if (nq <= 512)
+        FQ_LN_LAUNCH(512);
+    else
+        FQ_LN_LAUNCH(1024);
+#undef FQ_LN_LAUNCH
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}

@@ -17,6 +17,7 @@ exchange.  The gather / reduce logic is backend-agnostic and tested with gloo on
 (tests/test_dist.py).
 """
 import torch
+import numpy as np
 import torch.distributed as dist
 
 TILE = 16
@@ -192,6 +193,59 @@ def _ipc_open(handle, offset):
     return p.value, p.value + offset
 
 
+class _DevArray:
+    """__cuda_array_interface__ of a raw device allocation (torch.as_tensor wraps it without a copy)."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def _uncached_zeros(shape, dtype, dev):
+    """A zeroed device tensor in UNCACHED device memory (hipExtMallocWithFlags(hipDeviceMallocUncached)):
+    the gather buffers and flags that peers store into over xGMI are then never served from a stale
+    line of this GPU's L2.  Returns (tensor, raw pointer to hipFree) or (plain torch.zeros, None)
+    when the allocation or the wrapping is not available."""
+    import ctypes
+    import torch
+    nbytes = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+    try:
+        hip = _hip()
+        p = ctypes.c_void_p()
+        hip.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        if hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(nbytes), ctypes.c_uint(0x3)) != 0 or not p.value:
+            raise RuntimeError("hipExtMallocWithFlags(hipDeviceMallocUncached) failed")
+        if hip.hipMemset(p, 0, ctypes.c_size_t(nbytes)) != 0:
+            hip.hipFree(p)
+            raise RuntimeError("hipMemset failed")
+        typestr = {torch.float16: "<f2", torch.int32: "<i4"}[dtype]
+        t = torch.as_tensor(_DevArray(p.value, shape, typestr), device=dev)
+        if t.data_ptr() != p.value:
+            hip.hipFree(p)
+            raise RuntimeError("the tensor does not alias the allocation")
+        return t, p.value
+    except Exception:  # noqa: BLE001
+        return torch.zeros(shape, dtype=dtype, device=dev), None
+
+
+def _exportable_zeros(shape, dtype, dev):
+    """(tensor, raw uncached pointer or None, IPC export): uncached memory when it can be allocated,
+    wrapped and IPC-exported, else torch memory (every rank then reports `uncached` False)."""
+    import ctypes
+    import torch
+    t, raw = _uncached_zeros(shape, dtype, dev)
+    if raw is not None:
+        try:
+            torch.cuda.synchronize(dev)
+            return t, raw, _ipc_export(t)
+        except RuntimeError:
+            del t
+            _hip().hipFree(ctypes.c_void_p(raw))
+    t = torch.zeros(shape, dtype=dtype, device=dev)
+    torch.cuda.synchronize(dev)
+    return t, None, _ipc_export(t)
+
+
 class PeerGather:
     """Buffers of the fused peer-store all-gather (include/flexq_hip.h fq_linear_w6ax_gather): two
     gather buffers fp16 [M_max, N_total] per rank, used alternately, plus the rank's flag words, all
@@ -200,8 +254,12 @@ class PeerGather:
 
     `linear(x, image, abits)` runs this rank's column shard of a linear, stores it into every rank's
     gather buffer, waits until all ranks' shards have arrived and returns the full [M, N_total]
-    output (a view of this rank's gather buffer, valid until the call after next).  Replaces
-    ColumnParallelW6Linear's RCCL all_gather at decode sizes (M <= 32)."""
+    output, a view of this rank's gather buffer.  Lifetime: the output of call c must be consumed
+    (or copied) by work enqueued on the stream BEFORE this object's next linear() call.  After call
+    c + 1 a peer may already be at call c + 2, which stores into the same buffer parity as call c
+    (it only waits for every rank's call c + 1 flag), so reading output c after enqueuing call
+    c + 1 races with those stores.  Replaces ColumnParallelW6Linear's RCCL all_gather
+    at decode sizes (M <= 32).  The buffers and flags are uncached device memory (`uncached`)."""
 
     def __init__(self, M_max, N_total, group=None, device=None):
         import ctypes
@@ -215,12 +273,18 @@ class PeerGather:
         self.lo, self.hi = shard_range(N_total, self.world, self.rank)
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.dev = dev
-        self.bufs = [torch.zeros((M_max, N_total), dtype=torch.float16, device=dev) for _ in range(2)]
-        self.flags = torch.zeros(8, dtype=torch.int32, device=dev)
+        # the buffers peers store into, and the flags they raise, live in uncached device memory (no
+        # stale L2 line of this GPU can serve a read of a peer's xGMI store)
+        allocs = [_exportable_zeros((M_max, N_total), torch.float16, dev) for _ in range(2)]
+        allocs.append(_exportable_zeros((8,), torch.int32, dev))
+        self._raw = [a[1] for a in allocs if a[1] is not None]
+        self.uncached = len(self._raw) == 3
+        self.bufs = [allocs[0][0], allocs[1][0]]
+        self.flags = allocs[2][0]
         self.state = torch.zeros(2, dtype=torch.int32, device=dev)  # done, gen
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         torch.cuda.synchronize(dev)
-        mine = [_ipc_export(self.bufs[0]), _ipc_export(self.bufs[1]), _ipc_export(self.flags)]
+        mine = [a[2] for a in allocs]
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=group)
         self._opened = []
@@ -298,6 +362,8 @@ class PeerGather:
         return int(self.err.item())
 
     def close(self):
+        """Unmap the peers' buffers.  This rank's own uncached buffers stay allocated for the life of
+        the process: a captured graph may still name them, and peers may still hold mappings."""
         hip = _hip()
         import ctypes
         for p in self._opened:

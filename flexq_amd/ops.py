@@ -261,6 +261,56 @@ def silu_mul_quantize(gate, up, abits, return_act=False):
     return (xq, xs, act) if return_act else (xq, xs)
 
 
+def _vec_ok(t, name, K, dev):
+    if t is not None:
+        _dev(t, torch.float16, name, 1)
+        _need(t.numel() == K and t.device == dev, f"{name} must be [K] on the residual's device")
+
+
+def _span(t):
+    return (t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) if t is not None else None
+
+
+def _overlap(a, b):
+    a, b = _span(a), _span(b)
+    return a is not None and b is not None and a[0] < b[1] and b[0] < a[1]
+
+
+def layernorm_quantize(residual, gamma, abits, beta=None, eps=1e-5, input=None, bias=None, residual_out=None,
+                       return_normed=False):
+    """Residual [+ input] [+ bias] + LayerNorm (gamma, beta) + dynamic group quantization
+    (fq_layernorm_quantize; the reference's OPT-family generalAddBiasResidualLayerNormOpt2FlexQFusion,
+    layernorm_kernels.cu:316-575, and its pre-attention form, :2325-2420).  residual_out (fp16 [M,K],
+    may be the residual itself) receives half(residual + input + bias) when given.  Returns (xq int8
+    [M,K], xs fp16 [K/128, M]) (+ the fp16 normalised activations)."""
+    _dev(residual, torch.float16, "residual", 2)
+    M, K = residual.shape
+    _k_ok(K)
+    _need(K <= 32768, "K must be <= 32768")
+    dev = residual.device
+    _vec_ok(gamma, "gamma", K, dev)
+    _need(gamma is not None, "gamma is required")
+    _vec_ok(beta, "beta", K, dev)
+    _vec_ok(bias, "bias", K, dev)
+    if input is not None:
+        _dev(input, torch.float16, "input", 2)
+        _need(tuple(input.shape) == (M, K) and input.device == dev, "input must match residual")
+    if residual_out is not None:
+        _dev(residual_out, torch.float16, "residual_out", 2)
+        _need(tuple(residual_out.shape) == (M, K) and residual_out.device == dev, "residual_out must match residual")
+        for name, t in (("input", input), ("bias", bias), ("gamma", gamma), ("beta", beta)):
+            _need(not _overlap(residual_out, t), f"residual_out must not overlap {name}")
+        _need(residual_out.data_ptr() == residual.data_ptr() or not _overlap(residual_out, residual),
+              "residual_out must be the residual or not overlap it")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    xq = torch.empty((M, K), dtype=torch.int8, device=dev)
+    xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=dev)
+    normed = torch.empty((M, K), dtype=torch.float16, device=dev) if return_normed else None
+    _lib.call("fq_layernorm_quantize", _ptr(input), _ptr(residual), _ptr(bias), _ptr(residual_out), _ptr(gamma),
+              _ptr(beta), ctypes.c_float(eps), M, K, abits, _ptr(xq), _ptr(xs), _ptr(normed), _stream(residual))
+    return (xq, xs, normed) if return_normed else (xq, xs)
+
+
 def _act_scratch(fn, M, N, K, dev):
     if not int(getattr(_lib.load(), fn)(M, N, K)):
         return None, None  # the producer runs inside the decode GEMM: no activation scratch
@@ -298,7 +348,8 @@ def rmsnorm_linear_w6ax(residual, gamma, wpk, N, abits=6, eps=1e-6, input=None, 
             residual_out = torch.empty_like(residual)
         _dev(residual_out, torch.float16, "residual_out", 2)
         _need(tuple(residual_out.shape) == (M, K) and residual_out.device == dev, "residual_out must match residual")
-        _need(residual_out.data_ptr() != residual.data_ptr(), "residual_out must not be the residual")
+        for name, t in (("residual", residual), ("input", input), ("gamma", gamma)):
+            _need(not _overlap(residual_out, t), f"residual_out must not overlap {name}")
     else:
         residual_out = None
     out = _out_ok(out, M, N, dev)
@@ -309,6 +360,44 @@ def rmsnorm_linear_w6ax(residual, gamma, wpk, N, abits=6, eps=1e-6, input=None, 
               ctypes.c_float(eps), M, N, K, abits, _ptr(wpk), _ptr(out), _ptr(xq), _ptr(xs), _ptr(wbuf),
               ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
     return out, (residual_out if input is not None else residual)
+
+
+def layernorm_linear_w6ax(residual, gamma, wpk, N, abits=6, beta=None, eps=1e-5, input=None, bias=None,
+                          residual_out=None, out=None):
+    """Residual [+ input] [+ bias] + LayerNorm + quantize + W6Ax GEMM (fq_layernorm_linear_w6ax; the OPT
+    decoder's LayerNorm -> qkv / fc1 pair): one launch at decode sizes (M = 1, K = 4096), else
+    fq_layernorm_quantize + GEMM -- the same bits either way.  residual_out (optional; allocated when
+    input or bias is given and it is None) receives half(residual + input + bias); it must not
+    overlap the residual or any other input.  Returns (d fp16 [M, N], residual_out or None)."""
+    _dev(residual, torch.float16, "residual", 2)
+    M, K = residual.shape
+    _k_ok(K)
+    dev = residual.device
+    _vec_ok(gamma, "gamma", K, dev)
+    _need(gamma is not None, "gamma is required")
+    _vec_ok(beta, "beta", K, dev)
+    _vec_ok(bias, "bias", K, dev)
+    _img_ok(wpk, N, K)
+    _need(wpk.device == dev, "the weight image must be on the residual's device")
+    _need(abits in (6, 8), "abits must be 6 or 8")
+    if input is not None:
+        _dev(input, torch.float16, "input", 2)
+        _need(tuple(input.shape) == (M, K) and input.device == dev, "input must match residual")
+    if residual_out is None and (input is not None or bias is not None):
+        residual_out = torch.empty_like(residual)
+    if residual_out is not None:
+        _dev(residual_out, torch.float16, "residual_out", 2)
+        _need(tuple(residual_out.shape) == (M, K) and residual_out.device == dev, "residual_out must match residual")
+        for name, t in (("residual", residual), ("input", input), ("bias", bias), ("gamma", gamma), ("beta", beta)):
+            _need(not _overlap(residual_out, t), f"residual_out must not overlap {name}")
+    out = _out_ok(out, M, N, dev)
+    xq, xs = _act_scratch("fq_layernorm_linear_scratch_bytes", M, N, K, dev)
+    s = _stream(residual)
+    wbuf = workspace(dev, gemm_workspace_bytes(M, N, K), s.value)
+    _lib.call("fq_layernorm_linear_w6ax", _ptr(input), _ptr(residual), _ptr(bias), _ptr(residual_out), _ptr(gamma),
+              _ptr(beta), ctypes.c_float(eps), M, N, K, abits, _ptr(wpk), _ptr(out), _ptr(xq), _ptr(xs), _ptr(wbuf),
+              ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return out, residual_out
 
 
 def silu_linear_w6ax(gate, up, wpk, N, abits=8, out=None):

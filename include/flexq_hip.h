@@ -148,6 +148,22 @@ fq_status fq_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const u
 fq_status fq_silu_mul_quantize(const uint16_t *gate, const uint16_t *up, int ld, int M, int N,
                                int abits, int8_t *xq, uint16_t *xs, uint16_t *act_out,
                                fq_stream_t stream);
+/* OPT-family residual + bias + LayerNorm (mean and variance, gamma, beta) + dynamic group
+ * quantization, one launch.  Replaces generalAddBiasResidualLayerNormOpt2FlexQFusion
+ * (e2e .../kernels/layernorm_kernels.cu:316-575) and its pre-attention form
+ * invokeGeneralLayerNorm (:2325-2420: residual only):
+ *   v[m][k]        = ((0 + float(bias[k])) + float(residual[m][k])) + float(input[m][k])   (fp32;
+ *                    bias and input may be NULL: skipped)
+ *   res_out[m][k]  = half(v)            (optional; may be the residual itself, nothing else it reads)
+ *   mean, rs       = (s / (K/2)) / 2,  1 / sqrt(((q / (K/2)) / 2 - mean^2) + eps), s and q the
+ *                    row's fp32 sums of v and v^2 over half2 pairs (the build's fixed order)
+ *   normed[m][k]   = ((half(v) - half(mean)) * half(rs)) * gamma[k] [+ beta[k]], fp16 operations
+ *   xq, xs         = fq_quantize_act(normed, abits)
+ * normed_out optional.  K % 128 == 0, K <= 32768, 16-byte aligned rows. */
+fq_status fq_layernorm_quantize(const uint16_t *input, const uint16_t *residual, const uint16_t *bias,
+                                uint16_t *res_out, const uint16_t *gamma, const uint16_t *beta,
+                                float eps, int M, int K, int abits, int8_t *xq, uint16_t *xs,
+                                uint16_t *normed_out, fq_stream_t stream);
 
 /* ---- producer + linear in one call: the decoder layer's three W6Ax linears that follow a producer
  * (qkv and gate_up after the add-residual RMSNorm, down_proj after SiLU * up).  At decode sizes the
@@ -175,6 +191,18 @@ fq_status fq_silu_linear_w6ax(const uint16_t *gate, const uint16_t *up, int ld, 
                               int abits, const void *w_packed, uint16_t *d, int8_t *xq_buf,
                               uint16_t *xs_buf, void *workspace, size_t workspace_bytes,
                               fq_stream_t stream);
+/* fq_layernorm_linear_w6ax: d = linear(codes of LayerNorm(residual [+ input] [+ bias])), the OPT
+ *   decoder's LayerNorm -> qkv / fc1 pair (generalAddBiasResidualLayerNormOpt2FlexQFusion, then
+ *   FLEXQGEMMWrapper::gemm).  One launch when M == 1 and K == 4096 (the RMSNorm form's chunking);
+ *   otherwise fq_layernorm_quantize into xq_buf / xs_buf, then the GEMM.  residual_out (may be NULL)
+ *   receives half(v); in the one-launch form it must not be the residual (other workgroups still
+ *   read it) and must not overlap any input.  Bit-identical to fq_layernorm_quantize + fq_gemm_w6ax. */
+size_t fq_layernorm_linear_scratch_bytes(int M, int N, int K);
+fq_status fq_layernorm_linear_w6ax(const uint16_t *input, const uint16_t *residual, const uint16_t *bias,
+                                   uint16_t *residual_out, const uint16_t *gamma, const uint16_t *beta,
+                                   float eps, int M, int N, int K, int abits, const void *w_packed,
+                                   uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
+                                   size_t workspace_bytes, fq_stream_t stream);
 
 /* ---- column-parallel decode with the all-gather in the GEMM epilogue -------
  * The north-star N-shard: rank p of P holds columns [col0, col0 + N) of a linear whose full width is

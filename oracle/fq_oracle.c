@@ -393,6 +393,56 @@ long fqo_check_div_by_const(int hi) {
     return bad;
 }
 
+/* The device quantizer's element step (flexq_amd/csrc/fq_common.h quant_group16): instead of the
+ * IEEE quotient RN(x / s) rounded half away from zero, one fused multiply-add
+ *     t = RN(x * rcb + copysign(0.5, x)),  rcb = RN(rc * (1 + 2^-20)),  rc = v_rcp_f32(s) (1 ulp),
+ * truncated by v_cvt_i32_f32 (NaN -> 0, saturating) and clamped to [lo, hi].  x and s are fp16, so
+ * a quotient that is not an exact tie k + 0.5 lies well beyond the reciprocal's error from one,
+ * and the 2^-20 bias carries an exact tie across the truncation boundary.  This checks the claim
+ * exhaustively: every fp16 absmax a (0 .. inf), s = half(a / hi) as the engine forms it, the
+ * reciprocal rounded to nearest and moved by rc_ulp units in the last place, and every fp16 x
+ * with |x| <= a or x NaN.  Returns the number of codes that differ from the reference's.
+ * Test infrastructure only. */
+static int cvt_i32_sat_f(float v) {
+    if (isnan(v)) return 0;
+    if (v >= 2147483648.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (int)0x80000000u;
+    return (int)v; /* truncation */
+}
+long fqo_check_quant_fma(int bits, int rc_ulp) {
+    const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
+    const float bias = 1.0f + 0x1p-20f;
+    long bad = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : bad)
+    for (int ab = 0; ab <= 0x7c00; ab++) {
+        const float a = fqo_f16_to_f32((uint16_t)ab);
+        volatile float maxv = a / (float)hi;
+        const float r = fqo_f16_to_f32(fqo_f32_to_f16(maxv));
+        float rc = 1.0f / r;
+        if (isfinite(rc) && rc != 0.0f)
+            for (int k = 0; k < (rc_ulp < 0 ? -rc_ulp : rc_ulp); k++) rc = nextafterf(rc, rc_ulp < 0 ? 0.0f : INFINITY);
+        volatile float rcbv = rc * bias;
+        const float rcb = rcbv;
+        for (int xb = 0; xb < 65536; xb++) {
+            const uint16_t xa = (uint16_t)(xb & 0x7fff);
+            if (xa > ab && xa <= 0x7c00) continue; /* |x| > absmax cannot occur in the group */
+            const float x = fqo_f16_to_f32((uint16_t)xb);
+            volatile float qv = x / r;
+            const float v = round_half_away(qv);
+            int ref;
+            if (isnan(v)) ref = 0;
+            else if (v >= (float)hi) ref = hi;
+            else if (v <= (float)lo) ref = lo;
+            else ref = (int)v;
+            const float t = fmaf(x, rcb, copysignf(0.5f, x));
+            int c = cvt_i32_sat_f(t);
+            c = c < lo ? lo : (c > hi ? hi : c);
+            if (c != ref) bad++;
+        }
+    }
+    return bad;
+}
+
 /* ---------------------------------------------------------------- fused producers (§8(f)1) */
 
 /* clamp_inf_for_half (e2e .../kernels/reduce_kernel_utils.cuh:357-361): +-(65504 - 1000), then fp16 */
@@ -452,6 +502,86 @@ int fqo_rmsnorm_quantize(const uint16_t *input, uint16_t *residual, const uint16
         }
     }
     free(acc);
+    return fqo_quantize_engine(normed, M, K, bits, xq, xs);
+}
+
+/* 64-lane xor butterfly (offsets 1 .. 32) of one wave's values, then the waves in order: the bits of
+ * the kernels' wave_sum64 + cross-wave sum (flexq_amd/csrc/fq_common.h) */
+static float block_sum(const float *acc, int T) {
+    float total = 0.0f;
+    for (int w = 0; w < T / 64; w++) {
+        float lane[64];
+        for (int l = 0; l < 64; l++) lane[l] = acc[64 * w + l];
+        for (int off = 1; off <= 32; off <<= 1) {
+            float nxt[64];
+            for (int l = 0; l < 64; l++) nxt[l] = lane[l] + lane[l ^ off];
+            memcpy(lane, nxt, sizeof(lane));
+        }
+        total = w == 0 ? lane[0] : total + lane[0];
+    }
+    return total;
+}
+
+/* OPT-family residual + bias + LayerNorm + quantization, restating
+ * generalAddBiasResidualLayerNormOpt2FlexQFusion (e2e .../kernels/layernorm_kernels.cu:316-575) with
+ * this build's fixed summation order (flexq_amd/csrc/fq_common.h ln_add8 .. ln_apply8):
+ *   v = ((0 + bias) + residual) + input in fp32, absent terms skipped (:357-385); h = half(v) is the
+ *   residual output (:393-395); per half2 pair s += v0 + v1, q += v0*v0 + v1*v1 (:396-397), per thread
+ *   over its 8-value chunks c*T + t in order, then block_sum; mean = (s / (K/2)) / 2,
+ *   rs = 1 / sqrt(((q / (K/2)) / 2 - mean*mean) + eps) (:403-404, IEEE for rsqrtf);
+ *   normed = ((h - half(mean)) * half(rs)) * gamma [+ beta], each an fp16 operation (:412-416);
+ *   then the engine quantizer (:447-507).
+ * input, bias, beta may be NULL; res_out (may be NULL) receives h. */
+int fqo_layernorm_quantize(const uint16_t *input, const uint16_t *residual, const uint16_t *bias,
+                           uint16_t *res_out, const uint16_t *gamma, const uint16_t *beta, float eps, int M,
+                           int K, int bits, int8_t *xq, uint16_t *xs, uint16_t *normed) {
+    if (M <= 0 || K <= 0 || K % 128 || (bits != 6 && bits != 8)) return 1;
+    const int nq = K / 8, T = nq <= 256 ? 256 : nq <= 512 ? 512 : 1024;
+    float *sacc = (float *)malloc(sizeof(float) * T), *qacc = (float *)malloc(sizeof(float) * T);
+    uint16_t *h = (uint16_t *)malloc(sizeof(uint16_t) * K);
+    if (!sacc || !qacc || !h) return 2;
+    for (int m = 0; m < M; m++) {
+        const size_t row = (size_t)m * K;
+        for (int t = 0; t < T; t++) sacc[t] = qacc[t] = 0.0f;
+        for (int c = 0; c * T < nq; c++)
+            for (int t = 0; t < T; t++) {
+                const int q = c * T + t;
+                if (q >= nq) continue;
+                for (int e = 0; e < 8; e += 2) {
+                    float v[2];
+                    for (int u = 0; u < 2; u++) {
+                        const size_t k = 8 * (size_t)q + e + u;
+                        float a = 0.0f;
+                        if (bias) a = a + f16_to_f32(bias[k]);
+                        a = a + f16_to_f32(residual[row + k]);
+                        if (input) a = a + f16_to_f32(input[row + k]);
+                        v[u] = a;
+                        h[k] = fqo_f32_to_f16(a);
+                    }
+                    sacc[t] = sacc[t] + (v[0] + v[1]);
+                    volatile float p0 = v[0] * v[0], p1 = v[1] * v[1];
+                    qacc[t] = qacc[t] + (p0 + p1);
+                }
+            }
+        if (res_out) memcpy(res_out + row, h, sizeof(uint16_t) * K);
+        const float s = block_sum(sacc, T), qq = block_sum(qacc, T);
+        const float n = (float)(K / 2);
+        const float mean = (s / n) / 2.0f;
+        volatile float mm = mean * mean;
+        const float var = ((qq / n) / 2.0f - mm) + eps;
+        const float rs = 1.0f / sqrtf(var);
+        const double mh = f16_to_f32(fqo_f32_to_f16(mean)), rh = f16_to_f32(fqo_f32_to_f16(rs));
+        for (int k = 0; k < K; k++) {
+            double a = f16_to_f32(f64_to_f16(f16_to_f32(h[k]) - mh)); /* each step rounded to fp16 */
+            a = f16_to_f32(f64_to_f16(a * rh));
+            uint16_t o = f64_to_f16(a * f16_to_f32(gamma[k]));
+            if (beta) o = f64_to_f16((double)f16_to_f32(o) + f16_to_f32(beta[k]));
+            normed[row + k] = o;
+        }
+    }
+    free(sacc);
+    free(qacc);
+    free(h);
     return fqo_quantize_engine(normed, M, K, bits, xq, xs);
 }
 

@@ -46,6 +46,7 @@ def lib():
             "fqo_unpack_fq6": [P, I, I, P, P],
             "fqo_rmsnorm_quantize": [P, P, P, ctypes.c_float, I, I, I, P, P, P],
             "fqo_silu_mul_ref": [P, P, I, I, I, P],
+            "fqo_layernorm_quantize": [P, P, P, P, P, P, ctypes.c_float, I, I, I, P, P, P],
         }.items():
             fn = getattr(L, name)
             fn.argtypes = args
@@ -118,6 +119,26 @@ def rmsnorm_quantize(inp, residual, gamma, eps, bits):
     return res, normed, q, xs
 
 
+def layernorm_quantize(inp, residual, gamma, beta, eps, bits, bias=None):
+    """OPT-family bias + residual + input LayerNorm + engine quantizer (layernorm_kernels.cu:316-575,
+    the HIP kernel's summation order) -> (residual_out = half(v), normed fp16 [M,K], q int8 [M,K],
+    xs fp16 [K/128, M]).  inp, beta, bias may be None."""
+    res = np.ascontiguousarray(residual, dtype=np.float16)
+    M, K = res.shape
+    g = np.ascontiguousarray(gamma, dtype=np.float16)
+    b = None if beta is None else np.ascontiguousarray(beta, dtype=np.float16)
+    bi = None if bias is None else np.ascontiguousarray(bias, dtype=np.float16)
+    inp = None if inp is None else np.ascontiguousarray(inp, dtype=np.float16)
+    rout = np.zeros((M, K), dtype=np.float16)
+    normed = np.zeros((M, K), dtype=np.float16)
+    q = np.zeros((M, K), dtype=np.int8)
+    xs = np.zeros((K // 128, M), dtype=np.float16)
+    opt = lambda a: None if a is None else _p(a)  # noqa: E731
+    _check(lib().fqo_layernorm_quantize(opt(inp), _p(res), opt(bi), _p(rout), _p(g), opt(b), ctypes.c_float(eps),
+                                        M, K, bits, _p(q), _p(xs), _p(normed)), "layernorm_quantize")
+    return rout, normed, q, xs
+
+
 def silu_mul_ref(gate, up):
     """half(silu(gate) * up) evaluated in double (activation_kernels.cu:133,300)."""
     g = np.ascontiguousarray(gate, dtype=np.float16)
@@ -168,6 +189,16 @@ def check_div_by_const(hi):
     f.argtypes = [ctypes.c_int]
     f.restype = ctypes.c_long
     return int(f(hi))
+
+
+def check_quant_fma(bits, rc_ulp=0):
+    """Mismatches of the device quantizer's single-FMA element step (biased reciprocal, truncation)
+    against roundf(x / s) over every fp16 absmax and element, with the hardware reciprocal moved
+    by rc_ulp units in the last place (oracle/fq_oracle.c fqo_check_quant_fma); 0 = identical."""
+    f = lib().fqo_check_quant_fma
+    f.argtypes = [ctypes.c_int, ctypes.c_int]
+    f.restype = ctypes.c_long
+    return int(f(bits, rc_ulp))
 
 
 def fq6_bytes(N, K):

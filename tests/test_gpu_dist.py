@@ -84,7 +84,7 @@ def _peer_worker(rank, world, port, cases, q):
                 want.append(yr.cpu().numpy())
                 if K == N:
                     x = y.clone()                     # a dependent chain (next input = this output)
-            out[(M, N, K, abits)] = (got, want, pg.error())
+            out[(M, N, K, abits)] = (got, want, pg.error(), pg.uncached)
             pg.close()
         q.put((rank, out))
         dist.barrier()
@@ -114,8 +114,9 @@ def test_peer_store_gather_matches_all_gather(dev, world):
         assert p_.exitcode == 0
     for (M, N, K, abits, chain) in cases:
         for r in range(world):
-            got, want, err = res[r][(M, N, K, abits)]
+            got, want, err, uncached = res[r][(M, N, K, abits)]
             assert err == 0, f"rank {r}: a gather wait timed out"
+            assert uncached, f"rank {r}: the gather buffers are not in uncached device memory"
             assert len(got) == chain
             for i, (g, w) in enumerate(zip(got, want)):
                 np.testing.assert_array_equal(g.view(np.uint16), w.view(np.uint16), err_msg=f"rank {r} call {i}")

@@ -243,3 +243,110 @@ def test_fused_producer_linear_status_codes(ops, dev):
 def ctypes_size(n):
     import ctypes
     return ctypes.c_size_t(n)
+
+
+# ---- OPT-family LayerNorm producer (generalAddBiasResidualLayerNormOpt2FlexQFusion,
+# layernorm_kernels.cu:316-575): residual output, normalised fp16, codes and scales bit-exact against
+# oracle.layernorm_quantize (the kernel's summation order; fp16 elementwise steps as the reference)
+def _ln_inputs(M, K, seed, with_input, with_bias, with_beta):
+    r = rng(seed)
+    res = (r.standard_normal((M, K)) * 2.0 + 0.25).astype(np.float16)
+    inp = (r.standard_normal((M, K)) * 0.5).astype(np.float16) if with_input else None
+    bias = (0.1 * r.standard_normal(K)).astype(np.float16) if with_bias else None
+    gamma = (1.0 + 0.2 * r.standard_normal(K)).astype(np.float16)
+    beta = (0.05 * r.standard_normal(K)).astype(np.float16) if with_beta else None
+    res[0, :6] = [0.0, -0.0, 6e-8, -3e4, 3e4, 1e-3]
+    return res, inp, bias, gamma, beta
+
+
+@pytest.mark.parametrize("M,K", [(1, 4096), (3, 7168), (16, 4096), (5, 128), (2, 32768), (64, 9216), (2048, 4096)])
+@pytest.mark.parametrize("bits", [6, 8])
+@pytest.mark.parametrize("form", ["pre", "post", "post_nobias", "nobeta"])
+def test_layernorm_quantize_bit_exact(ops, dev, M, K, bits, form):
+    """pre: invokeGeneralLayerNorm's FlexQ form (residual only); post: bias + residual + input (the
+    post-attention add, layernorm_kernels.cu:357-385); without bias; without beta."""
+    with_input, with_bias, with_beta = {"pre": (False, False, True), "post": (True, True, True),
+                                        "post_nobias": (True, False, True), "nobeta": (True, True, False)}[form]
+    res, inp, bias, gamma, beta = _ln_inputs(M, K, M * 31 + K + bits, with_input, with_bias, with_beta)
+    eps = 1e-5
+    d = lambda a: None if a is None else to_dev(a, dev)  # noqa: E731
+    res_d = d(res)
+    rout = torch.empty_like(res_d)
+    xq, xs, normed = ops.layernorm_quantize(res_d, d(gamma), bits, beta=d(beta), eps=eps, input=d(inp),
+                                            bias=d(bias), residual_out=rout, return_normed=True)
+    r_ref, n_ref, q_ref, xs_ref = oracle.layernorm_quantize(inp, res, gamma, beta, eps, bits, bias=bias)
+    np.testing.assert_array_equal(hbits(host(rout)), hbits(r_ref), err_msg="residual out")
+    np.testing.assert_array_equal(hbits(host(normed)), hbits(n_ref), err_msg="normed")
+    np.testing.assert_array_equal(host(xq), q_ref, err_msg="codes")
+    np.testing.assert_array_equal(hbits(host(xs)), hbits(xs_ref), err_msg="scales")
+    np.testing.assert_array_equal(hbits(host(res_d)), hbits(res), err_msg="the residual must not change")
+
+
+def test_layernorm_quantize_in_place(ops, dev):
+    """residual_out may be the residual itself (each thread owns its chunks)."""
+    res, inp, bias, gamma, beta = _ln_inputs(4, 4096, 3, True, True, True)
+    res_d = to_dev(res, dev)
+    xq, xs = ops.layernorm_quantize(res_d, to_dev(gamma, dev), 6, beta=to_dev(beta, dev), input=to_dev(inp, dev),
+                                    bias=to_dev(bias, dev), residual_out=res_d)
+    r_ref, _, q_ref, _ = oracle.layernorm_quantize(inp, res, gamma, beta, 1e-5, 6, bias=bias)
+    np.testing.assert_array_equal(hbits(host(res_d)), hbits(r_ref))
+    np.testing.assert_array_equal(host(xq), q_ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (1, 12288, 4096), (1, 16384, 4096), (1, 256, 4096),
+                                   (1, 4096, 7168), (4, 4096, 4096), (16, 1024, 9216)])
+@pytest.mark.parametrize("form", ["pre", "post"])
+def test_layernorm_linear_matches_producer_then_gemm(ops, dev, M, N, K, form):
+    """fq_layernorm_linear_w6ax (LayerNorm inside the decode GEMM's prologue at M = 1, K = 4096: the
+    OPT-6.7B width) against fq_layernorm_quantize + fq_gemm_w6ax: output and residual output
+    bit-identical, the inputs untouched; and the output against the CPU oracle."""
+    from common import assert_gemm_close
+    post = form == "post"
+    res, inp, bias, gamma, beta = _ln_inputs(M, K, M * 13 + N + K, post, post, True)
+    eps = 1e-5
+    wpk = _image(ops, dev, N, K, 8)
+    d = lambda a: None if a is None else to_dev(a, dev)  # noqa: E731
+    res_d, g_d, b_d, inp_d, bias_d = d(res), d(gamma), d(beta), d(inp), d(bias)
+    fused_expected = M == 1 and K == 4096 and ops.gemm_workspace_bytes(M, N, K) == 0
+    assert (int(ops._lib.load().fq_layernorm_linear_scratch_bytes(M, N, K)) == 0) == fused_expected
+    rout = torch.empty_like(res_d)
+    y, h = ops.layernorm_linear_w6ax(res_d, g_d, wpk, N, 6, beta=b_d, eps=eps, input=inp_d, bias=bias_d,
+                                     residual_out=rout)
+    rout2 = torch.empty_like(res_d)
+    xq, xs = ops.layernorm_quantize(res_d, g_d, 6, beta=b_d, eps=eps, input=inp_d, bias=bias_d, residual_out=rout2)
+    y2 = ops.gemm_w6ax(xq, xs, wpk, N, 6)
+    np.testing.assert_array_equal(hbits(host(y)), hbits(host(y2)), err_msg="output")
+    np.testing.assert_array_equal(hbits(host(h)), hbits(host(rout2)), err_msg="residual out")
+    np.testing.assert_array_equal(hbits(host(res_d)), hbits(res), err_msg="the residual must not change")
+    _, _, q_ref, xs_ref = oracle.layernorm_quantize(inp, res, gamma, beta, eps, 6, bias=bias)
+    wq, ws = ops.unpack_w6(wpk, N, K)
+    ref, _, mag = oracle.gemm(q_ref, xs_ref, host(wq), host(ws))
+    assert_gemm_close(host(y), ref, mag, "layernorm_linear vs oracle")
+
+
+def test_producer_linear_alias_rejections(ops, dev):
+    """The one-launch forms write residual_out while other workgroups still read their inputs:
+    residual_out overlapping the residual, the input or gamma is refused, for RMSNorm
+    and LayerNorm alike, through the C ABI and the Python wrappers."""
+    from flexq_amd import _lib
+    lib = _lib.load()
+    K, N = 4096, 256
+    buf = torch.zeros(3 * K, dtype=torch.float16, device=dev)
+    res, inp = buf[:K].view(1, K), buf[K:2 * K].view(1, K)
+    gamma = torch.ones(K, dtype=torch.float16, device=dev)
+    wpk = _image(ops, dev, N, K, 9)
+    d = torch.empty((1, N), dtype=torch.float16, device=dev)
+    s, ptr, z = ops._stream(res), ops._ptr, ctypes_size(0)
+    for bad in (inp, buf[K + 8:2 * K + 8].view(1, K), res):  # input, overlapping the input, the residual
+        assert lib.fq_rmsnorm_linear_w6ax(ptr(inp), ptr(res), ptr(bad), ptr(gamma), 1e-6, 1, N, K, 6, ptr(wpk),
+                                          ptr(d), None, None, None, z, s) == 2
+        assert lib.fq_layernorm_linear_w6ax(ptr(inp), ptr(res), None, ptr(bad), ptr(gamma), None, 1e-5, 1, N, K, 6,
+                                            ptr(wpk), ptr(d), None, None, None, z, s) == 2
+    g16 = torch.zeros(K, dtype=torch.float16, device=dev)
+    assert lib.fq_rmsnorm_linear_w6ax(ptr(inp), ptr(res), ptr(g16), ptr(g16), 1e-6, 1, N, K, 6, ptr(wpk), ptr(d),
+                                      None, None, None, z, s) == 2
+    with pytest.raises(ValueError):
+        ops.rmsnorm_linear_w6ax(res, gamma, wpk, N, input=inp, residual_out=inp)
+    with pytest.raises(ValueError):
+        ops.layernorm_linear_w6ax(res, gamma, wpk, N, input=inp, residual_out=res)
+    torch.cuda.synchronize()

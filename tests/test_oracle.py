@@ -206,3 +206,13 @@ def test_quantizer_division_by_constant_is_exact(hi):
     """The device quantizer replaces absmax / (2^(b-1)-1) by a Newton-corrected product with the
     rounded reciprocal constant; over every fp16 absmax it is bit-identical to IEEE division."""
     assert oracle.check_div_by_const(hi) == 0
+
+
+@pytest.mark.parametrize("bits", [6, 8])
+@pytest.mark.parametrize("rc_ulp", [0, 1, -1, 4, -4])
+def test_quantizer_fma_rounding_is_exact(bits, rc_ulp):
+    """The device quantizer's element step -- trunc(RN(x * rcb + copysign(0.5, x))) with the
+    reciprocal of the fp16 scale biased by 2^-20 -- gives roundf(x / s)'s code for every fp16
+    absmax and every element of such a group, whatever the hardware reciprocal's last bits
+    (v_rcp_f32 is within 1 ulp; checked to 4)."""
+    assert oracle.check_quant_fma(bits, rc_ulp) == 0

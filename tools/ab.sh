@@ -1,0 +1,37 @@
+#!/bin/bash
+# A/B of library builds in one run (development): every build timed REPS times, alternating, so
+# clock and box drift hit every arm alike.  Replaces the per-experiment ab_*.sh stubs.
+#
+#   tools/ab.sh MODE REPS LIB [LIB ...]
+#
+# MODE
+#   step     the headline bench step (LLaMA-2-7B, M = 1): ms/step and per-launch us
+#   m16      the batch-16 step (--config llama2-7b-m16): ms/step
+#   e2e      the 32-layer decoder step at M = 1 and 16 (bench decoder_layers_e2e)
+#   shapes   graph-timed decode launches (tools/shape_sweep.py; SHAPES="N K ...", M=..., FQ_SWEEP=...)
+#   prefill  prefill GEMMs (tools/prefill_bench.py at PF_M, default 16384)
+# Libraries are selected with FLEXQ_AMD_LIB / FQ_LIB (flexq_amd/_lib.py); build variants with
+#   make -C flexq_amd/csrc variant NAME=x DEFS="-DFOO=1"   ->  tools/libflexq_hip_x.so
+set -o pipefail
+MODE=$1; REPS=$2; shift 2
+[ -n "$MODE" ] && [ -n "$REPS" ] && [ $# -ge 1 ] || { sed -n 2,16p "$0"; exit 2; }
+B="python3 -u bench.py --cpu-budget 0 --no-fp16-compare --no-calibrate"
+J='import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1])'
+for rep in $(seq "$REPS"); do
+  for L in "$@"; do
+    printf "%s " "$L"
+    case $MODE in
+      step)    FLEXQ_AMD_LIB=$L timeout -k 10 200 $B --no-layers --no-extra-configs 2>/dev/null |
+                 python3 -c "$J; print(d['ms_per_step'], d['roofline']['per_launch_us'])" || exit 1 ;;
+      m16)     FLEXQ_AMD_LIB=$L timeout -k 10 300 $B --no-layers --no-extra-configs --config llama2-7b-m16 2>/dev/null |
+                 python3 -c "$J; print(d['ms_per_step'], d['roofline']['per_launch_us'])" || exit 1 ;;
+      e2e)     FLEXQ_AMD_LIB=$L timeout -k 10 300 $B --no-extra-configs --steps 5 --warmup 2 2>/dev/null |
+                 python3 -c "$J; e=d['decoder_layers_e2e']; print(e['M1']['w6_ms_per_step'], e['M16']['w6_ms_per_step'])" || exit 1 ;;
+      shapes)  echo; FQ_LIB=$L timeout -k 10 150 python3 -u tools/shape_sweep.py ${M:-1} ${SHAPES:-4096 4096 12288 4096 22016 4096 4096 11008} 2>&1 |
+                 grep "us/launch" || exit 1 ;;
+      prefill) echo; FQ_REPS=${FQ_REPS:-6} FQ_LIB=$L timeout -k 10 200 python3 tools/prefill_bench.py ${PF_M:-16384} 2>&1 |
+                 grep -E "^M=" | sed -E 's/\| linear.*//' || exit 1 ;;
+      *) echo "unknown mode $MODE"; exit 2 ;;
+    esac
+  done
+done
