@@ -130,13 +130,18 @@ def build_stack(cfg, rank, world, dev, merge=True, seed=1234, peer=False):
             src = prev if name != "up" else L["gate"]["x"].view(-1)
             x = src[:M * K].view(M, K)
             L[name] = dict(N=N, Nl=Nl, K=K, abits=abits, pk=pk, out=out, full=full, x=x)
+            if M >= ops.PREFILL_U8_MIN_M:  # prefill: the weights' int8 MFMA operands kept resident
+                L[name]["w_u8"] = ops.prepare_prefill_weights(pk, Nl, K)
             if peer and world > 1:
                 from flexq_amd.dist import PeerGather
                 if N not in gathers:
                     gathers[N] = [PeerGather(M, N, device=dev), 0]
                 pg, uses = gathers[N]
                 full = pg.bufs[uses & 1].view(-1)
-                L[name].update(pg=pg, parity=uses & 1, full=full)
+                # fold this linear's wait for its input into its launch when the input is the previous
+                # linear's gather buffer (merged gate_up: the chain is linear) and the buffers are uncached
+                L[name].update(pg=pg, parity=uses & 1, full=full,
+                               fold=bool(merge and pg.uncached and (stack or L) and name != "up"))
                 gathers[N][1] = uses + 1
             if name != "gate":
                 prev = (full if world > 1 else out).view(-1)
@@ -153,11 +158,17 @@ def run_step(stack, M, world, group=None, gather=True, staged=False):
     """One token through the linear stack, one launch per linear: fq_linear_w6ax (decode sizes:
     one fused quantize+GEMM launch each), then one RCCL all-gather of the fp16 shard outputs per
     linear when world > 1 (staged: through host memory, for the gloo rehearsal of --share-gpu)."""
-    for name, p in linears(stack):
+    lins_ = linears(stack)
+    for i, (name, p) in enumerate(lins_):
         if world > 1 and gather and "pg" in p:  # the all-gather fused into the GEMM epilogue
-            p["pg"].linear(p["x"], p["pk"], p["abits"], parity=p["parity"])
+            # each linear reads the previous one's gather buffer: that gather's wait is folded into
+            # this launch (after=...), only the step's last output gets a wait launch
+            prev = lins_[i - 1][1] if i > 0 else None
+            after = (prev["pg"], prev["parity"]) if prev is not None and "pg" in prev and p.get("fold") else None
+            p["pg"].linear(p["x"], p["pk"], p["abits"], parity=p["parity"], after=after,
+                           wait=not (i + 1 < len(lins_) and lins_[i + 1][1].get("fold")))
             continue
-        ops.linear_w6ax(p["x"], p["pk"], p["Nl"], p["abits"], out=p["out"])
+        ops.linear_w6ax(p["x"], p["pk"], p["Nl"], p["abits"], out=p["out"], w_u8=p.get("w_u8"))
         if world > 1 and gather:
             if staged:
                 full = torch.empty(p["full"].shape, dtype=p["full"].dtype)
@@ -612,7 +623,10 @@ def measure_single(ctx, name, merge, steps, warmup):
     replay = ctx.prepare(lambda: run_step(stack, M, 1), not ctx.a.no_graph)
     elapsed, ev_s = ctx.timed(replay, steps, warmup)
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)
-    out = {"what": f"BASELINE config: {desc}, the dependent linear stack of every layer, one HIP graph",
+    out = {"what": f"BASELINE config: {desc}, the dependent linear stack of every layer, one HIP graph" +
+                   (" (weights: the fq6 image + its int8 MFMA operands unpacked once at load, "
+                    "ops.prepare_prefill_weights; per linear the activation quantize + the prefill GEMM)"
+                    if M >= ops.PREFILL_U8_MIN_M else ""),
            "ms_per_step": round(elapsed / steps * 1e3, 4),
            "value": round(flops_step * steps / elapsed / 1e12, 4), "unit": "TFLOPS-equiv",
            "tok_per_s": round(M * steps / elapsed, 2), "steps": steps, "warmup": warmup,
@@ -625,7 +639,8 @@ def measure_single(ctx, name, merge, steps, warmup):
 
         def gemms():
             for nm, p in linears(stack):
-                ops.gemm_w6ax(codes[nm][0], codes[nm][1], p["pk"], p["Nl"], p["abits"], out=p["out"])
+                ops.gemm_w6ax(codes[nm][0], codes[nm][1], p["pk"], p["Nl"], p["abits"], out=p["out"],
+                              w_u8=p.get("w_u8"))
         _, per_gemm_s = ctx.graph_time(gemms, n_lin, 2)
         ops_launch = layers * sum(2.0 * M * N * K for (_, N, K, _) in launch_lins) / n_lin
         ach = ops_launch / per_gemm_s / 1e12
@@ -872,7 +887,8 @@ def main():
 
             def gemms():
                 for name, p in linears(stack):
-                    ops.gemm_w6ax(codes[name][0], codes[name][1], p["pk"], p["Nl"], p["abits"], out=p["out"])
+                    ops.gemm_w6ax(codes[name][0], codes[name][1], p["pk"], p["Nl"], p["abits"], out=p["out"],
+                                  w_u8=p.get("w_u8"))
 
             _, per_gemm_s = ctx.graph_time(gemms, n_lin, a.roofline_reps)
             ops_launch = layers * sum(2.0 * M * N * K for (_, N, K, _) in launch_lins) / n_lin

@@ -64,6 +64,10 @@ _SIGS = {
     "fq_rmsnorm_quantize": ([P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),
     "fq_silu_mul_quantize": ([P, P, I, I, I, I, P, P, P, P], I),
     "fq_layernorm_quantize": ([P, P, P, P, P, P, ctypes.c_float, I, I, I, P, P, P, P], I),
+    "fq_prefill_weight_bytes": ([I, I], SZ),
+    "fq_linear_w6ax_gather_after": ([P, P, P, I, I, I, I, P, P, P, P, P, SZ, P], I),
+    "fq_prefill_unpack_weights": ([P, I, I, P, P], I),
+    "fq_gemm_w6ax_u8": ([P, P, P, P, I, I, I, I, P, P, P, SZ, P], I),
     "fq_linear_w6ax_gather": ([P, I, I, I, I, P, P, P, P, P, SZ, P], I),
     "fq_gather_wait": ([P, P, P], I),
     "fq_rmsnorm_linear_scratch_bytes": ([I, I, I], SZ),

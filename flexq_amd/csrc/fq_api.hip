@@ -3,7 +3,8 @@
 
 fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
                                  uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
-                                 hipStream_t s, bool *launched, const fq_gather *gat);
+                                 hipStream_t s, bool *launched, const fq_gather *gat,
+                                 const fq_gather *wgat = nullptr, uint32_t *werr = nullptr);
 fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
                             int abits, uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
                             fq_stream_t stream, const fq_gather *gat);
@@ -64,6 +65,25 @@ extern "C" fq_status fq_linear_w6ax_gather(const uint16_t *x, int M, int N, int 
     if (st != FQ_OK) return st;
     return fq_gemm_w6ax_impl(xq_buf, xs_buf, w_packed, M, N, K, abits, nullptr, nullptr, workspace,
                              workspace_bytes, stream, gather);
+}
+
+// The gather kernel with the previous gather's wait folded into its prologue (one launch) where the
+// linear fuses its quantizer; otherwise fq_gather_wait, then fq_linear_w6ax_gather.
+extern "C" fq_status fq_linear_w6ax_gather_after(const uint16_t *x, const fq_gather *in_gather, uint32_t *err, int M,
+                                                 int N, int K, int abits, const void *w_packed,
+                                                 const fq_gather *gather, int8_t *xq_buf, uint16_t *xs_buf,
+                                                 void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+    if (!x || !w_packed || !gather || !in_gather) return FQ_ERR_NULL;
+    if (M <= 0 || M > 32 || N <= 0 || N % 16 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    bool launched = false;
+    fq_status st = fq_decode_linear_fused(x, M, N, K, abits, w_packed, nullptr, nullptr, workspace, workspace_bytes,
+                                          (hipStream_t)stream, &launched, gather, in_gather, err);
+    if (launched || st != FQ_OK) return st;
+    st = fq_gather_wait(in_gather, err, stream);
+    if (st != FQ_OK) return st;
+    return fq_linear_w6ax_gather(x, M, N, K, abits, w_packed, gather, xq_buf, xs_buf, workspace, workspace_bytes,
+                                 stream);
 }
 
 static bool overlaps(const void *a, size_t na, const void *b, size_t nb) {

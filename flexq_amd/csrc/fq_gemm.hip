@@ -142,8 +142,40 @@ __device__ __forceinline__ void gather_publish(const fq_gather *__restrict__ gat
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the fence's own wait can be dropped)
             for (int q = 0; q < gat->P; q++)
                 __hip_atomic_store(gat->flags[q] + gat->rank, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // this call's generation: the consumer (fq_gather_wait, or the next linear's prologue,
+            // gather_poll) waits for every rank's flag to reach it
+            __hip_atomic_store(gat->gen, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// The wait of a peer-store gather folded into the next linear's prologue (fq_linear_w6ax_gather_after):
+// wave 0 polls this rank's P flag words -- lane q rank q's word, system-scope loads of the uncached
+// flag array, s_sleep between polls -- until every one has reached the gather's generation (raised
+// by its last publish), while the linear's weight-ring DMAs, issued before, are in flight; the other
+// waves wait at a raw s_barrier (it does not drain their DMAs).  No acquire fence: the gather
+// buffers are uncached device memory (flexq_amd/dist.py PeerGather), stored system-scope and
+// drained by every peer before its flag, so a load issued after the poll matched reads the data
+// (an acquire's vmcnt(0) would also wait for the ring).  Bounded like fq_gather_wait: ~1 s, then the
+// error word is set and the launch goes on (results undefined, never a hang); once it is set, later
+// polls return at once.  Every wave of the workgroup must call it.
+__device__ __forceinline__ void gather_poll(const fq_gather *__restrict__ g, uint32_t *__restrict__ err, int wid) {
+    if (wid == 0) {
+        const int lane = threadIdx.x & 63;
+        if (!(err && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+            const uint32_t target = __hip_atomic_load(g->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t *mine = g->flags[g->rank];
+            bool ok = lane >= g->P;
+            for (int spin = 0; spin < (1 << 20); spin++) {
+                if (!ok) ok = __hip_atomic_load(mine + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target;
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (__builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0 && err)
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    __builtin_amdgcn_s_barrier();
 }
 
 // ---- deferred split-K fix-up of the decode kernels.  Every item's partial tile went out as
@@ -528,7 +560,10 @@ __device__ __forceinline__ void decode_body(
     // waiting for the window is vmcnt(D*U + nws).  Each wave instruction costs the CU's address
     // unit ~30 cycles whatever its size, and the prologue burst of all waves is ~60 of them: the
     // first-needed ones go first.
-    if (FUSE && n > 0) x_fetch(0);
+    // the peer-store gather kernel whose x is the previous gather's output: its wait is folded in
+    // here (gather_poll), after the ring is issued; the activation window follows the poll
+    const bool wfold = GAT && FUSE && pro.wgat != nullptr;
+    if (FUSE && n > 0 && !wfold) x_fetch(0);
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
     auto advance = [&]() {
         if (++rj == ng) {
@@ -548,9 +583,16 @@ __device__ __forceinline__ void decode_body(
         }
     }
     FQ_STAMP(1);
+    if (GAT && FUSE && wfold) {
+        gather_poll(pro.wgat, pro.werr, wid);
+        if (n > 0) x_fetch(0);
+    }
 
     if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
-        wait_vm_plus<D * C::U>(nws);
+        if (GAT && wfold)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the window was issued after the ring)
+        else
+            wait_vm_plus<D * C::U>(nws);
         FQ_STAMP(5);
         if (PRO == 1) {  // residual add + RMSNorm over the row (R = 4 pairs: lane = chunk 64 wid + lane)
             const uint32_t xb = lds_addr(xh_st) + lane * 16;
@@ -873,9 +915,12 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_gather_k
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d,
     const fq_gather *__restrict__ gat, float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW,
-    int RC, int xwin, int iq, int ir, int NCH) {
+    int RC, int xwin, int iq, int ir, int NCH, const fq_gather *__restrict__ wgat, uint32_t *__restrict__ werr) {
+    DecodePro pro{};
+    pro.wgat = wgat;
+    pro.werr = werr;
     decode_body<MT, XS, SS, FUSE, false, 0, false, 0, true>(xq, xs, xh, abits, wpk, Mall, N, K, d, nullptr, slabs,
-                                                            tickets, S, IPW, RC, xwin, iq, ir, NCH, gat, DecodePro{});
+                                                            tickets, S, IPW, RC, xwin, iq, ir, NCH, gat, pro);
 }
 #undef FQ_DECODE_ARGS
 #undef FQ_DECODE_PASS
@@ -923,7 +968,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ln_kerne
 __global__ __launch_bounds__(64) void fq_gather_wait_kernel(const fq_gather *__restrict__ gat, uint32_t *__restrict__ err) {
     const int lane = threadIdx.x;
     if (err && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
-    const uint32_t target = __hip_atomic_load(gat->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const uint32_t target = __hip_atomic_load(gat->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (publish advanced it)
     const uint32_t *mine = gat->flags[gat->rank];
     bool ok = lane >= gat->P;
     for (int spin = 0; spin < (1 << 20); spin++) {  // ~1 s at ~1 us per poll
@@ -936,7 +981,6 @@ __global__ __launch_bounds__(64) void fq_gather_wait_kernel(const fq_gather *__r
         return;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
-    if (lane == 0) __hip_atomic_store(gat->gen, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // =============================================================================================
@@ -1870,7 +1914,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
             hipLaunchKernelGGL((fq_gemm_decode_gather_kernel<MT, XS, SS, FUSE>), grid, block, lds, stream, a.xq, a.xs,
                                a.xh, a.abits, (const uint32_t *)a.wpk, a.M, a.N, a.K, a.d, a.gat, slabs, tickets, p.S,
                                p.IPW, p.RC, p.xwin, p.NT * p.S / (p.grid / p.NCH), p.NT * p.S % (p.grid / p.NCH),
-                               p.NCH);
+                               p.NCH, FUSE ? a.pro.wgat : nullptr, a.pro.werr);
             FQ_LAUNCH_CHECK();
             return FQ_OK;
         }
@@ -1934,13 +1978,17 @@ extern "C" size_t fq_linear_act_scratch_bytes(int M, int N, int K) {
 // One-launch decode linear (quantize + GEMM) when the staged plan fits; FQ_ERR_SHAPE otherwise.
 fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abits, const void *w_packed,
                                  uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
-                                 hipStream_t s, bool *launched, const fq_gather *gat) {
+                                 hipStream_t s, bool *launched, const fq_gather *gat, const fq_gather *wgat,
+                                 uint32_t *werr) {
     *launched = false;
     DecodePlan p;
     if (!decode_fuse(M, N, K, &p)) return FQ_OK;
     const size_t need = fq_gemm_workspace_bytes(M, N, K);
     if (need && (!workspace || workspace_bytes < need)) return FQ_ERR_WORKSPACE;
     DecodeArgs a = {nullptr, nullptr, x, abits, w_packed, M, N, K, d, acc_dbg, workspace, gat, DecodePro{}};
+    if (wgat && (!gat || acc_dbg)) return FQ_ERR_SHAPE;  // (the folded wait exists in the gather kernel only)
+    a.pro.wgat = wgat;
+    a.pro.werr = werr;
     *launched = true;
     return acc_dbg ? dispatch_decode<true, true>(p, a, s) : dispatch_decode<true, false>(p, a, s);
 }
@@ -2048,6 +2096,50 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
     return fq_gemm_w6ax_impl(xq, xs, w_packed, M, N, K, abits, d, acc_dbg, workspace, workspace_bytes, stream, nullptr);
 }
 
+// The prefill GEMM over once-unpacked int8 B operands wu ([NT][G][k-step][lane][16 B], written by
+// fq_unpack_w8_kernel): the 256 x 256 tile kernel, or the 128 x 128 one when its last-round fill is
+// better (M >= PF_U8_MIN_M).
+static fq_status launch_prefill_u8(const int8_t *xq, const uint16_t *xs, const void *w_packed, const char *wu, int M,
+                                   int N, int K, uint16_t *d, int32_t *acc_dbg, hipStream_t s) {
+    const int NT = (N + 15) / 16;
+    const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
+    const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
+    const size_t lds_big = 2 * (size_t)(PB_ASTAGE + PB_BSTAGE);
+    const bool xsf = M % PB_BM == 0;
+    // 256 x 256 or 128 x 128 tiles over the unpacked weights: the larger tile is ~13 % cheaper
+    // per MAC on a full chip, the smaller one fills it in finer steps (one WG per CU for 256 x
+    // 256, two for 128 x 128).  Take the 128 x 128 kernel when its last-round fill beats the
+    // 256 x 256 one's by more than that (tools/ab_pfm.sh, M = 2048 .. 8192 on the LLaMA-3-8B
+    // shapes: e.g. M = 2048, N = 4096: 128 WGs of 256 x 256 = half the CUs, 91 -> 69 us).
+    const double slots = device_cus();
+    const double fill_big = nbig / (ceil(nbig / slots) * slots), fill_128 = nwg / (ceil(nwg / (2 * slots)) * 2 * slots);
+    bool small_tiles = fill_big * 1.15 < fill_128;
+#ifdef FQ_DEV_ABLATION
+    if (const char *e = getenv("FQ_DEV_PF128")) small_tiles = atoi(e) != 0;  // development: force either
+#endif
+    if (small_tiles) {
+        if (acc_dbg)
+            hipLaunchKernelGGL((fq_gemm_prefill_kernel<true, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
+        else
+            hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
+        FQ_LAUNCH_CHECK();
+        return FQ_OK;
+    }
+#define FQ_BIG(dbg, xf)                                                                                  \
+    hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
+                       xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu)
+    if (acc_dbg) {
+        if (xsf) FQ_BIG(true, true); else FQ_BIG(true, false);
+    } else {
+        if (xsf) FQ_BIG(false, true); else FQ_BIG(false, false);
+    }
+#undef FQ_BIG
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
 fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
                             int abits, uint16_t *d, int32_t *acc_dbg, void *workspace, size_t workspace_bytes,
                             fq_stream_t stream, const fq_gather *gat) {
@@ -2120,41 +2212,8 @@ fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_
         char *wu = (char *)workspace + kTicketBytes;
         hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0, s,
                            (const char *)w_packed, nblk, wu);
-        const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
-        const size_t lds_big = 2 * (size_t)(PB_ASTAGE + PB_BSTAGE);
-        const bool xsf = M % PB_BM == 0;
-        // 256 x 256 or 128 x 128 tiles over the unpacked weights: the larger tile is ~13 % cheaper
-        // per MAC on a full chip, the smaller one fills it in finer steps (one WG per CU for 256 x
-        // 256, two for 128 x 128).  Take the 128 x 128 kernel when its last-round fill beats the
-        // 256 x 256 one's by more than that (tools/ab_pfm.sh, M = 2048 .. 8192 on the LLaMA-3-8B
-        // shapes: e.g. M = 2048, N = 4096: 128 WGs of 256 x 256 = half the CUs, 91 -> 69 us).
-        const double slots = device_cus();
-        const double fill_big = nbig / (ceil(nbig / slots) * slots), fill_128 = nwg / (ceil(nwg / (2 * slots)) * 2 * slots);
-        bool small_tiles = fill_big * 1.15 < fill_128;
-#ifdef FQ_DEV_ABLATION
-        if (const char *e = getenv("FQ_DEV_PF128")) small_tiles = atoi(e) != 0;  // development: force either
-#endif
-        if (small_tiles) {
-            if (acc_dbg)
-                hipLaunchKernelGGL((fq_gemm_prefill_kernel<true, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
-                                   xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
-            else
-                hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
-                                   xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
-            FQ_LAUNCH_CHECK();
-            return FQ_OK;
-        }
-#define FQ_BIG(dbg, xf)                                                                                  \
-        hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
-                           xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu)
-        if (acc_dbg) {
-            if (xsf) FQ_BIG(true, true); else FQ_BIG(true, false);
-        } else {
-            if (xsf) FQ_BIG(false, true); else FQ_BIG(false, false);
-        }
-#undef FQ_BIG
         FQ_LAUNCH_CHECK();
-        return FQ_OK;
+        return launch_prefill_u8(xq, xs, w_packed, wu, M, N, K, d, acc_dbg, s);
     }
     // Few tiles (narrow N, modest M): split K over more WGs when the workspace holds the slabs
     // (without the slabs the kernel would have to fall back to S = 1, whose fp32 summation order,
@@ -2178,6 +2237,37 @@ fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_
         FQ_LAUNCH_CHECK();
     }
     return FQ_OK;
+}
+
+// ---- prefill with resident unpacked weights: the int8 B operands of fq_unpack_w8_kernel kept for
+// the model's lifetime (1 byte per weight, 4/3 of the fq6 image) instead of unpacked on every call
+extern "C" size_t fq_prefill_weight_bytes(int N, int K) {
+    if (N <= 0 || K <= 0 || K % FQ_GROUP) return 0;
+    return prefill_u8_bytes(N, K);
+}
+
+extern "C" fq_status fq_prefill_unpack_weights(const void *w_packed, int N, int K, void *w_u8, fq_stream_t stream) {
+    if (!w_packed || !w_u8) return FQ_ERR_NULL;
+    if (N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    const long nblk = (long)((N + 15) / 16) * (K / FQ_GROUP);
+    hipLaunchKernelGGL(fq_unpack_w8_kernel, dim3((unsigned)((nblk * 64 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const char *)w_packed, nblk, (char *)w_u8);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+
+extern "C" fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8,
+                                     int M, int N, int K, int abits, uint16_t *d, int32_t *acc_dbg, void *workspace,
+                                     size_t workspace_bytes, fq_stream_t stream) {
+    if (!xq || !xs || !w_packed || !w_u8 || !d) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    if (M < PF_U8_MIN_M)  // (decode and mid-M plans do not read unpacked operands: the same bits)
+        return fq_gemm_w6ax(xq, xs, w_packed, M, N, K, abits, d, acc_dbg, workspace, workspace_bytes, stream);
+    const int NT = (N + 15) / 16;
+    const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
+    if (nwg > 0x7fffffffL) return FQ_ERR_SHAPE;
+    return launch_prefill_u8(xq, xs, w_packed, (const char *)w_u8, M, N, K, d, acc_dbg, (hipStream_t)stream);
 }
 
 extern "C" fq_status fq_gather_wait(const fq_gather *gather, uint32_t *err, fq_stream_t stream) {

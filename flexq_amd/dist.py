@@ -331,10 +331,15 @@ class PeerGather:
         dist.barrier(group=group)  # every rank's buffers are mapped before anyone stores into them
         self.calls = 0
 
-    def linear(self, x, image, abits=6, parity=None):
+    def linear(self, x, image, abits=6, parity=None, after=None, wait=True):
         """x fp16 [M, K] (replicated) -> full output [M, N_total] (this rank's gather buffer).
         parity: which of the two gather buffers (default: alternate per call); a caller capturing
-        a fixed sequence of calls (a HIP graph) passes it explicitly, alternating per object."""
+        a fixed sequence of calls (a HIP graph) passes it explicitly, alternating per object.
+        after=(pg, parity): x is the output of that PeerGather call, issued with wait=False: its
+        wait runs inside this launch (fq_linear_w6ax_gather_after: after the weight DMAs, no wait
+        launch) when both objects' buffers are uncached, else as fq_gather_wait first.
+        wait=False: skip this call's own wait -- the caller must pass after=(self, parity) to the
+        next linear that reads this output (or call wait(parity) before reading it otherwise)."""
         import ctypes
         import torch
         from . import _lib, ops
@@ -352,10 +357,27 @@ class PeerGather:
         if ops.act_scratch_bytes(M, n, K):
             xq = torch.empty((M, K), dtype=torch.int8, device=x.device)
             xs = torch.empty((K // GROUP, M), dtype=torch.float16, device=x.device)
-        _lib.call("fq_linear_w6ax_gather", ops._ptr(x), M, n, K, abits, ops._ptr(image), ops._ptr(self.desc[parity]),
-                  ops._ptr(xq), ops._ptr(xs), ops._ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
-        _lib.call("fq_gather_wait", ops._ptr(self.desc[parity]), ops._ptr(self.err), s)
+        wsz = ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0)
+        if after is not None:
+            src, sp = after
+            if self.uncached and src.uncached:
+                _lib.call("fq_linear_w6ax_gather_after", ops._ptr(x), ops._ptr(src.desc[sp]), ops._ptr(src.err), M, n,
+                          K, abits, ops._ptr(image), ops._ptr(self.desc[parity]), ops._ptr(xq), ops._ptr(xs),
+                          ops._ptr(wbuf), wsz, s)
+            else:
+                src.wait(sp, x)
+                after = None
+        if after is None:
+            _lib.call("fq_linear_w6ax_gather", ops._ptr(x), M, n, K, abits, ops._ptr(image),
+                      ops._ptr(self.desc[parity]), ops._ptr(xq), ops._ptr(xs), ops._ptr(wbuf), wsz, s)
+        if wait:
+            self.wait(parity, x)
         return self.bufs[parity][:M]
+
+    def wait(self, parity, like):
+        """fq_gather_wait for this object's latest call (the stream of tensor `like`)."""
+        from . import _lib, ops
+        _lib.call("fq_gather_wait", ops._ptr(self.desc[parity]), ops._ptr(self.err), ops._stream(like))
 
     def error(self):
         """Nonzero when a wait timed out (a rank stopped publishing)."""

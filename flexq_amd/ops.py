@@ -153,9 +153,24 @@ def quantize_act(x, abits):
 
 # ------------------------------------------------------------------------- GEMM
 
-def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None):
+PREFILL_U8_MIN_M = 2048  # fq_gemm_w6ax unpacks the weights (once per call) at and above this M
+
+
+def prepare_prefill_weights(wpk, N, K):
+    """The weight image's int8 MFMA operands, unpacked once (fq_prefill_unpack_weights; 1 byte per
+    weight): pass them as gemm_w6ax / linear_w6ax(..., w_u8=) so that prefill-sized calls skip the
+    per-call unpack pass.  A uint8 tensor owned by the caller (the model), on the image's device."""
+    _img_ok(wpk, N, K)
+    nb = int(_lib.load().fq_prefill_weight_bytes(N, K))
+    w_u8 = torch.empty(nb, dtype=torch.uint8, device=wpk.device)
+    _lib.call("fq_prefill_unpack_weights", _ptr(wpk), N, K, _ptr(w_u8), _stream(wpk))
+    return w_u8
+
+
+def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None, w_u8=None):
     """d fp16 [M,N] from quantized operands; with return_acc also the int32 group accumulators
-    [M, N, K/128] (bit-exact debug output)."""
+    [M, N, K/128] (bit-exact debug output).  w_u8: the prepared operands of prepare_prefill_weights
+    (fq_gemm_w6ax_u8; bit-identical, no per-call unpack at M >= 2048)."""
     _dev(xq, torch.int8, "xq", 2)
     M, K = xq.shape
     _k_ok(K)
@@ -173,6 +188,13 @@ def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None):
         _need(tuple(out.shape) == (M, N), "out shape mismatch")
     acc = torch.empty((M, N, K // GROUP), dtype=torch.int32, device=dev) if return_acc else None
     s = _stream(xq)
+    if w_u8 is not None and M >= PREFILL_U8_MIN_M:
+        _dev(w_u8, torch.uint8, "w_u8", 1)
+        _need(w_u8.numel() >= int(_lib.load().fq_prefill_weight_bytes(N, K)) and w_u8.device == dev,
+              "w_u8 must be prepare_prefill_weights(wpk, N, K) on the operands' device")
+        _lib.call("fq_gemm_w6ax_u8", _ptr(xq), _ptr(xs), _ptr(wpk), _ptr(w_u8), M, N, K, abits, _ptr(out),
+                  _ptr(acc), None, ctypes.c_size_t(0), s)
+        return (out, acc) if return_acc else out
     nb = gemm_workspace_bytes(M, N, K)
     wbuf = workspace(dev, nb, s.value)
     _lib.call("fq_gemm_w6ax", _ptr(xq), _ptr(xs), _ptr(wpk), M, N, K, abits, _ptr(out),
@@ -180,8 +202,9 @@ def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None):
     return (out, acc) if return_acc else out
 
 
-def linear_w6ax(x, wpk, N, abits=6, out=None):
-    """Quantize + GEMM (FLEXQGEMMWrapper::gemm(const half* A ...)) for fp16 x [M,K]."""
+def linear_w6ax(x, wpk, N, abits=6, out=None, w_u8=None):
+    """Quantize + GEMM (FLEXQGEMMWrapper::gemm(const half* A ...)) for fp16 x [M,K].  w_u8: the
+    prepared operands of prepare_prefill_weights (prefill sizes: quantize + fq_gemm_w6ax_u8)."""
     _dev(x, torch.float16, "x", 2)
     M, K = x.shape
     _k_ok(K)
@@ -194,6 +217,9 @@ def linear_w6ax(x, wpk, N, abits=6, out=None):
     else:
         _dev(out, torch.float16, "out", 2)
         _need(tuple(out.shape) == (M, N), f"out must be [M, N] = {(M, N)}")
+    if w_u8 is not None and M >= PREFILL_U8_MIN_M:
+        xq, xs = quantize_act(x, abits)
+        return gemm_w6ax(xq, xs, wpk, N, abits, out=out, w_u8=w_u8)
     xq = xs = None
     if act_scratch_bytes(M, N, K):  # prefill sizes quantize in a separate launch
         xq = torch.empty((M, K), dtype=torch.int8, device=dev)

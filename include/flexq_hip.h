@@ -125,6 +125,20 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
                          uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                          size_t workspace_bytes, fq_stream_t stream);
 
+/* ---- prefill with resident unpacked weights ------------------------------------------------------
+ * At M >= 2048 fq_gemm_w6ax unpacks the weight image into int8 MFMA operands in its workspace on
+ * every call (fq_unpack_w8_kernel: 0.75 B read + 1 B written per weight).  A caller that keeps the
+ * unpacked operands for the model's lifetime (1 byte per weight) skips that pass:
+ * fq_prefill_unpack_weights writes them once (w_u8 of fq_prefill_weight_bytes(N, K) bytes, 256-byte
+ * aligned) and fq_gemm_w6ax_u8 runs the prefill GEMM over them -- bit-identical to fq_gemm_w6ax; below
+ * M = 2048 it IS fq_gemm_w6ax (those plans do not read unpacked operands).  The reference has no
+ * prefill kernel (its BLOCK_M <= 8 tiles re-stream W, flexq_bmma_op.h:111-114). */
+size_t fq_prefill_weight_bytes(int N, int K);
+fq_status fq_prefill_unpack_weights(const void *w_packed, int N, int K, void *w_u8, fq_stream_t stream);
+fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8, int M,
+                          int N, int K, int abits, uint16_t *d, int32_t *acc_dbg, void *workspace,
+                          size_t workspace_bytes, fq_stream_t stream);
+
 /* ---- fused producers of the activation codes ---------------------------- */
 /* Residual add + RMSNorm (T5 / LLaMA style: no mean, no bias) + dynamic group quantization, one
  * launch.  Replaces generalAddResidualT5LayerNormFlexQFusion / invokeGeneralAddResidualT5PreLayerNorm
@@ -210,8 +224,8 @@ fq_status fq_layernorm_linear_w6ax(const uint16_t *input, const uint16_t *residu
  * them straight into EVERY rank's gather buffer out[q] (fp16 [M][ld], IPC-mapped device pointers:
  * xGMI peer stores on a node), with system-scope write-through stores; after the launch's last
  * workgroup has seen every store drained it raises flags[q][rank] = *gen + 1 in every rank.
- * fq_gather_wait (one small launch) then waits for all P flags of this rank, acquires and advances
- * *gen: after it, out[rank] holds the whole [M][ld] output.  This replaces the per-linear RCCL
+ * The last workgroup also advances *gen to that value; fq_gather_wait (one small launch) then waits
+ * for all P flags of this rank and acquires: after it, out[rank] holds the whole [M][ld] output.  This replaces the per-linear RCCL
  * all_gather (nccl_utils.cc:70-82's ftNcclAllGather in the reference) at decode sizes.
  * Use two gather buffers alternately (linear j writes buffer j % 2): a rank can then run at most
  * one linear ahead of any other without overwriting an input still being read.  The struct lives
@@ -231,6 +245,18 @@ fq_status fq_linear_w6ax_gather(const uint16_t *x, int M, int N, int K, int abit
                                 const fq_gather *gather, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                                 size_t workspace_bytes, fq_stream_t stream);
 fq_status fq_gather_wait(const fq_gather *gather, uint32_t *err, fq_stream_t stream);
+/* fq_linear_w6ax_gather whose input x is the output of in_gather (this rank's gather buffer of the
+ * previous linear), with that gather's wait folded into the launch: the kernel issues its weight
+ * DMAs, then one wave polls in_gather's flags (system-scope loads; bounded like fq_gather_wait, err
+ * = in_gather's error word) and the activation is read after the poll.  Requires the gather buffers
+ * and flags in uncached device memory (hipExtMallocWithFlags(hipDeviceMallocUncached): no acquire
+ * fence, so no stale cache line may serve the reads).  One launch where fq_linear_w6ax would fuse its
+ * quantizer; otherwise fq_gather_wait(in_gather) then fq_linear_w6ax_gather.  Bit-identical to the
+ * two-call form.  The generation advances at each publish, so either wait form may follow any call. */
+fq_status fq_linear_w6ax_gather_after(const uint16_t *x, const fq_gather *in_gather, uint32_t *err, int M, int N,
+                                      int K, int abits, const void *w_packed, const fq_gather *gather,
+                                      int8_t *xq_buf, uint16_t *xs_buf, void *workspace, size_t workspace_bytes,
+                                      fq_stream_t stream);
 
 /* ---- reference-layout entry points (drop-in for FlexQ's own formats) ------------------------ */
 /* flexq_bit_packing(const int* in, int* out, M, K, BIT, stream) (engine/src/pack/bit_packing.h:34,

@@ -84,7 +84,21 @@ def _peer_worker(rank, world, port, cases, q):
                 want.append(yr.cpu().numpy())
                 if K == N:
                     x = y.clone()                     # a dependent chain (next input = this output)
-            out[(M, N, K, abits)] = (got, want, pg.error(), pg.uncached)
+            # the folded form (K == N): every call reads the previous call's gather buffer in place and
+            # waits for it inside its own launch (fq_linear_w6ax_gather_after), no wait launches, no
+            # host synchronisation inside the chain; only the last output is waited for
+            folded = []
+            if K == N:
+                x0 = torch.from_numpy(act_input(M, K, seed=32).astype(np.float16)).to(dev)
+                pg2 = fqd.PeerGather(M, N, device=dev)
+                y = pg2.linear(x0, img, abits, parity=0, wait=False)
+                for step in range(1, chain):
+                    y = pg2.linear(y, img, abits, parity=step & 1, after=(pg2, (step - 1) & 1), wait=False)
+                pg2.wait((chain - 1) & 1, y)
+                torch.cuda.synchronize()
+                folded = [y.cpu().numpy().copy(), pg2.error()]
+                pg2.close()
+            out[(M, N, K, abits)] = (got, want, pg.error(), pg.uncached, folded)
             pg.close()
         q.put((rank, out))
         dist.barrier()
@@ -97,7 +111,10 @@ def test_peer_store_gather_matches_all_gather(dev, world):
     """fq_linear_w6ax_gather + fq_gather_wait (the all-gather fused into the decode GEMM epilogue
     through IPC-mapped peer buffers) against ColumnParallelW6Linear's all_gather: every rank's full
     output bit-identical to the collective's, over dependent chains of calls that alternate the two
-    gather buffers, at M = 1 (fused quantizer), M = 4 (split-K shard) and M = 16 (separate quantize)."""
+    gather buffers, at M = 1 (fused quantizer), M = 4 (split-K shard) and M = 16 (separate quantize);
+    and the same chains with each wait folded into the next call (fq_linear_w6ax_gather_after: one
+    launch per linear where the quantizer is fused, the wait launch first elsewhere) bit-identical
+    to the two-launch chain's last output."""
     import torch.multiprocessing as mp
     cases = [(1, 2048, 2048, 6, 6), (4, 512, 8192, 8, 3), (16, 4096, 4096, 6, 4)]
     with socket.socket() as s_:
@@ -114,9 +131,13 @@ def test_peer_store_gather_matches_all_gather(dev, world):
         assert p_.exitcode == 0
     for (M, N, K, abits, chain) in cases:
         for r in range(world):
-            got, want, err, uncached = res[r][(M, N, K, abits)]
+            got, want, err, uncached, folded = res[r][(M, N, K, abits)]
             assert err == 0, f"rank {r}: a gather wait timed out"
             assert uncached, f"rank {r}: the gather buffers are not in uncached device memory"
+            if folded:  # the folded chain ends where the two-launch chain ends, bit for bit
+                assert folded[1] == 0, f"rank {r}: a folded gather wait timed out"
+                np.testing.assert_array_equal(folded[0].view(np.uint16), got[-1].view(np.uint16),
+                                              err_msg=f"rank {r}: folded chain")
             assert len(got) == chain
             for i, (g, w) in enumerate(zip(got, want)):
                 np.testing.assert_array_equal(g.view(np.uint16), w.view(np.uint16), err_msg=f"rank {r} call {i}")
@@ -136,7 +157,7 @@ def test_gather_wait_times_out_once_then_fails_fast(dev):
         _fields_ = [("out", P8), ("flags", P8), ("done", ctypes.c_uint64), ("gen", ctypes.c_uint64), ("ints", I4)]
     buf = torch.zeros((1, 16), dtype=torch.float16, device=dev)
     flags = torch.zeros(8, dtype=torch.int32, device=dev)  # never raised
-    state = torch.zeros(2, dtype=torch.int32, device=dev)
+    state = torch.tensor([0, 1], dtype=torch.int32, device=dev)  # generation 1 was published by this rank
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     d = Desc()
     d.out[0], d.flags[0] = buf.data_ptr(), flags.data_ptr()
@@ -149,7 +170,7 @@ def test_gather_wait_times_out_once_then_fails_fast(dev):
     _lib.call("fq_gather_wait", ops._ptr(desc), ops._ptr(err), s)
     torch.cuda.synchronize()
     t1 = time.time()
-    assert int(err.item()) == 1 and int(state[1].item()) == 0  # timed out, generation not advanced
+    assert int(err.item()) == 1 and int(state[1].item()) == 1  # timed out; the wait never moves the generation
     assert 0.05 < t1 - t0 < 30, t1 - t0
     for _ in range(20):
         _lib.call("fq_gather_wait", ops._ptr(desc), ops._ptr(err), s)

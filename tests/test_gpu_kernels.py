@@ -61,6 +61,57 @@ def test_quantize_act_edge_cases(ops, dev, bits):
     np.testing.assert_array_equal(host(xq), oracle.quantize_engine(x, 6)[0])
 
 
+def special_value_input():
+    """Rows of 8 groups mixing NaN (alone, beside inf, in every lane position), +-inf, -0, all-
+    subnormal groups, fp16 max and ordinary values: the quantizer's integer absmax fast path and its
+    NaN fallback (a wave where any group holds a NaN) against the oracle."""
+    r = rng(77)
+    K = 1024
+    x = (r.standard_normal((12, K)) * 2.0).astype(np.float16)
+    nan, inf = np.float16(np.nan), np.float16(np.inf)
+    x[0, 5] = nan                                       # one NaN, the rest of the row ordinary
+    x[1, 128:256:7] = nan                               # many NaNs in one group
+    x[2, 300] = inf
+    x[3, 400], x[3, 401] = -inf, nan                    # NaN and inf in one group
+    x[4, :128] = -0.0
+    x[4, 128:256] = 0.0
+    x[4, 256:384] = np.ldexp(r.integers(-1023, 1024, 128).astype(np.float64), -24).astype(np.float16)
+    x[5, :] = np.float16(65504.0) * np.where(r.random(K) < 0.5, 1, -1).astype(np.float16)
+    x[6, 700] = -inf
+    x[6, 900] = nan
+    x[7, ::128] = nan                                   # a NaN leading every group
+    x[8, 127::128] = inf                                # an inf closing every group
+    x[9] = np.ldexp(r.integers(-1023, 1024, K).astype(np.float64), -24).astype(np.float16)  # subnormals
+    x[10, 0] = np.float16(6.1e-5)                       # smallest normal beside subnormals
+    x[10, 1:128] = np.ldexp(r.integers(-1023, 1024, 127).astype(np.float64), -24).astype(np.float16)
+    x[11, 640:768] = np.frombuffer(np.uint16(0x7e01).tobytes() * 128, np.float16)  # NaN payloads only
+    return x
+
+
+@pytest.mark.parametrize("bits", [6, 8])
+def test_quantize_act_special_values(ops, dev, bits):
+    x = special_value_input()
+    q_ref, xs_ref = oracle.quantize_engine(x, bits)
+    xq, xs = ops.quantize_act(to_dev(x, dev), bits)
+    np.testing.assert_array_equal(host(xq), q_ref)
+    np.testing.assert_array_equal(host(xs).view(np.uint16), xs_ref.view(np.uint16))
+    # NaN-free rows alone (every wave on the fast path) give the same codes as beside the NaN rows
+    clean = [i for i in range(x.shape[0]) if not np.isnan(x[i]).any()]
+    xq2, xs2 = ops.quantize_act(to_dev(x[clean], dev), bits)
+    np.testing.assert_array_equal(host(xq2), q_ref[clean])
+    # the fused decode quantizer (M = 1 linear) is the same code: same outputs as the separate
+    # quantize + GEMM on the oracle's codes (NaN/inf outputs where a scale is inf, in the same places)
+    N = 64
+    wq = rng(6).integers(-32, 32, size=(N, x.shape[1])).astype(np.int8)
+    ws = (rng(7).random((x.shape[1] // 128, N)) * 0.05).astype(np.float16)
+    pk = ops.pack_w6(to_dev(wq, dev), to_dev(ws, dev))
+    for i in range(x.shape[0]):
+        d = ops.linear_w6ax(to_dev(x[i:i + 1], dev), pk, N, bits)
+        d2 = ops.gemm_w6ax(to_dev(q_ref[i:i + 1], dev), to_dev(np.ascontiguousarray(xs_ref[:, i:i + 1]), dev),
+                           pk, N, bits)
+        np.testing.assert_array_equal(host(d), host(d2), err_msg=f"row {i}")
+
+
 def tie_heavy_input(M, K, bits, seed):
     """Groups whose scale is exactly a power of two s (absmax = (2^(b-1)-1) s), every other value
     an integer multiple of s/2: about half the quotients are exact .5 ties, the rest exact
@@ -540,6 +591,33 @@ def test_prefill_unpacked_path_bit_identical(ops, dev, M, N, K):
     torch.cuda.synchronize()
     assert torch.equal(a1, a2)
     assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 1000, 1280), (16384, 1004, 1280), (4096, 4096, 4096), (1000, 512, 1280),
+                                   (32, 4096, 4096)])
+def test_prefill_resident_weights_bit_identical(ops, dev, M, N, K):
+    """fq_prefill_unpack_weights once + fq_gemm_w6ax_u8 (the caller keeps the int8 operands) against
+    fq_gemm_w6ax (unpacking per call in its workspace): identical fp16 outputs and int32
+    accumulators; below M = 2048 (and at decode sizes) the _u8 entry is fq_gemm_w6ax itself.  The
+    linear wrapper with w_u8 gives the same bits as without."""
+    g = torch.Generator(device=dev).manual_seed(M + 3 * N)
+    xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    w_u8 = ops.prepare_prefill_weights(pk, N, K)
+    assert w_u8.numel() == ((N + 15) // 16) * (K // 128) * 2048
+    d1, a1 = ops.gemm_w6ax(xq, xs, pk, N, 8, return_acc=True)
+    d2, a2 = ops.gemm_w6ax(xq, xs, pk, N, 8, return_acc=True, w_u8=w_u8)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2)
+    assert torch.equal(d1.view(torch.int16), d2.view(torch.int16))
+    x = (torch.randn((M, K), device=dev, generator=g)).half()
+    y1 = ops.linear_w6ax(x, pk, N, 8)
+    y2 = ops.linear_w6ax(x, pk, N, 8, w_u8=w_u8)
+    torch.cuda.synchronize()
+    assert torch.equal(y1.view(torch.int16), y2.view(torch.int16))
 
 
 # The round-1 prefill kernel with VGPR-destination asm loads faulted on one shape of this list
