@@ -53,6 +53,10 @@ _SIGS = {
     "fq_gemm_w6ax": ([P, P, P, I, I, I, I, P, P, P, SZ, P], I),
     "fq_linear_w6ax": ([P, I, I, I, I, P, P, P, P, P, SZ, P], I),
     "fq_linear_act_scratch_bytes": ([I, I, I], SZ),
+    "fq_linear_chain_w6ax": ([P, I, I, P, SZ, P, P, P, SZ, P], I),
+    "fq_chain_workspace_init": ([P, SZ, P], I),
+    "fq_chain_error_offset": ([], SZ),
+    "fq_chain_workspace_bytes": ([P, I, I], SZ),
     "fq_ref_bit_packing": ([P, P, I, I, I, P], I),
     "fq_ref_quantize_bit_packing": ([P, P, P, I, I, I, P], I),
     "fq_import_ref_w": ([P, P, I, I, P, P], I),

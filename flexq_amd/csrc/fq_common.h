@@ -91,10 +91,12 @@ __device__ __forceinline__ int cvt_i32_sat(float v) {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-// The f32 path: absmax over the values converted to fp32 (fmaxf skips NaN, as the reference's __hmax),
-// the element step on the converted values.  quant_group16 takes it for a wave where some group
-// holds a NaN (rare); it is bit-identical to the fast path everywhere else.
-__device__ __forceinline__ uint16_t quant_group16_f32(uint4 raw, int bits, uint2 &codes) {
+// One (row, 128-group) per 16 lanes, 8 fp16 values per lane: absmax over the values converted to
+// fp32 (fmaxf skips NaN, as the reference's __hmax), the element step on the converted values.
+// (An integer-absmax variant -- a packed-u16 max over the fp16 bit patterns, one conversion instead
+// of eight, v_fma_mix element steps, a NaN fallback -- was bit-identical and 0.8-1.1 % slower per
+// step: DESIGN.md §8.)
+__device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &codes) {
     const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
     const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
     v2f v[4];
@@ -144,66 +146,6 @@ __device__ __forceinline__ uint16_t quant_group16_f32(uint4 raw, int bits, uint2
 
 __device__ __forceinline__ float lo_f(uint32_t w) { return h2f((uint16_t)w); }
 __device__ __forceinline__ float hi_f(uint32_t w) { return h2f((uint16_t)(w >> 16)); }
-
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-
-// low bytes of 8 codes -> 2 dwords (v_perm_b32: selector 0x0c = zero byte)
-__device__ __forceinline__ uint2 pack_codes8(const int (&c)[8]) {
-    uint32_t w[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)c[4 * h + 1], (uint32_t)c[4 * h], 0x0c0c0400u);
-        const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)c[4 * h + 3], (uint32_t)c[4 * h + 2], 0x0c0c0400u);
-        w[h] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
-    }
-    return make_uint2(w[0], w[1]);
-}
-
-// The fast path (every group of the wave NaN-free):
-//   absmax: |x| as fp16 bit patterns order like unsigned integers (+0 .. inf = 0x7c00, NaN above), so
-//           the group's absmax is a packed-u16 max over the lane's 8 values and a 16-lane integer DPP
-//           max -- one conversion to fp32 instead of eight; a maximum above 0x7c00 flags a NaN, and
-//           the wave then takes quant_group16_f32 (wave-uniform branch);
-//   element: t = v_fma_mix_f32(x_f16, rcb, copysign(0.5, x)_f16), the 0.5 of x's sign formed for two
-//           halves at once ((x & 0x80008000) | 0x38003800); the same fused multiply-add as the f32
-//           path (f16 operands convert exactly), so the same codes.
-#ifndef FQ_QUANT_FAST
-#define FQ_QUANT_FAST 1
-#endif
-__device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &codes) {
-    if (!FQ_QUANT_FAST) return quant_group16_f32(raw, bits, codes);
-    const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
-    const int hi = (1 << (bits - 1)) - 1, lo = -(1 << (bits - 1));
-    us2 a[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) a[i] = __builtin_bit_cast(us2, wd[i] & 0x7fff7fffu);
-    const us2 m2 = __builtin_elementwise_max(__builtin_elementwise_max(a[0], a[1]), __builtin_elementwise_max(a[2], a[3]));
-    int mb = max((int)m2.x, (int)m2.y);
-    mb = max(mb, dpp_i32<0xB1>(mb));
-    mb = max(mb, dpp_i32<0x4E>(mb));
-    mb = max(mb, dpp_i32<0x141>(mb));
-    mb = max(mb, dpp_i32<0x140>(mb));
-    if (__builtin_amdgcn_ballot_w64(mb > 0x7c00) != 0) return quant_group16_f32(raw, bits, codes);
-    const float mx = h2f((uint16_t)mb);
-    // IEEE fp32 absmax / hi as a Newton-corrected product with y = RN(1/hi): bit-identical over
-    // every fp16 absmax (exhaustive: tests/test_oracle.py::test_quantizer_division_by_constant_is_exact)
-    const float fhi = (float)hi, y = bits == 8 ? (float)(1.0 / 127.0) : (float)(1.0 / 31.0);
-    const float m1 = mx * y;
-    const float maxv = __builtin_isfinite(m1) ? fmaf(fmaf(-m1, fhi, mx), y, m1) : m1;
-    const uint16_t sh = f2h(maxv);
-    // element step and its proof: quant_group16_f32 above
-    const float rcb = __builtin_amdgcn_rcpf(h2f(sh)) * (1.0f + 0x1p-20f);
-    int c[8];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t hs = (wd[i] & 0x80008000u) | 0x38003800u;  // +-0.5 with the sign of each half
-        const float t0 = fmaf(lo_f(wd[i]), rcb, lo_f(hs)), t1 = fmaf(hi_f(wd[i]), rcb, hi_f(hs));
-        c[2 * i] = med3_i32(cvt_i32_sat(t0), lo, hi);
-        c[2 * i + 1] = med3_i32(cvt_i32_sat(t1), lo, hi);
-    }
-    codes = pack_codes8(c);
-    return sh;
-}
 
 // ---- producer arithmetic, 8 fp16 values per call: fq_producers.hip's kernels and the decode
 // kernel's fused prologues (fq_gemm.hip, PRO = 1 / 2 / 4) share these, so the two give the same bits.
@@ -368,6 +310,11 @@ struct DecodePro {
     const uint16_t *bias;   // PRO 4 (or null)
     const struct fq_gather *wgat;  // peer-store gather kernel: the gather whose output is x, waited
     uint32_t *werr;                //   for in the prologue (or null: x is ready); its error word
+    uint32_t *chain;        // decode chain (fq_linear_chain_w6ax): the launch's sync words
+    int link;               //   this linear's position in the chain
+    uint32_t epoch;         //   the launch's epoch (granule tags)
+    const uint64_t *hx;     //   granules holding x (the previous linear's hand-off), or null: x is ready
+    uint64_t *hd;           //   this linear's hand-off granules (null: the chain's last linear)
 };
 
 // ---- fq6 weight unpack ----------------------------------------------------------------------

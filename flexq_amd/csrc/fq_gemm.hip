@@ -178,6 +178,63 @@ __device__ __forceinline__ void gather_poll(const fq_gather *__restrict__ g, uin
     __builtin_amdgcn_s_barrier();
 }
 
+// ---- decode chain (fq_linear_chain_w6ax): consecutive dependent linears in ONE persistent launch,
+// one workgroup per CU.  Linear l + 1 issues its weight ring and w-scale staging (which depend on
+// nothing) first and only then waits for its activations, so the wait hides under the first blocks
+// of its stream instead of sitting behind a kernel boundary (~1.75 us) and the next
+// launch's ramp.
+// Hand-off: data-tagged 8-byte granules {two fp16 outputs, tag} (MI355X_MICROARCH.md price list,
+// granule rows; R2: a granule is one naturally aligned 8-byte sc1 store and needs no ordering).  A
+// linear whose output feeds the next one writes each pair of outputs twice: to the caller's d, and
+// as a granule into its hand-off buffer in the workspace.  The consumer's waves load their own
+// activation slices from that buffer with sc1 buffer loads and re-load until every granule carries
+// the expected tag -- no flag, no counter, no drain, no second round trip for the data.
+// The hand-off buffers live in the chain workspace (fq_chain_workspace_init), which nothing but
+// chain launches writes: zero at first, then granules of earlier launches.  Tag = E + 1, E = the
+// epoch word every workgroup reads as the launch starts (a run's hand-off buffers are disjoint), so
+// no granule an earlier launch left matches.  Every workgroup adds 1 to its shard of a start counter
+// after reading E; workgroup 0, in linear 1's prologue, waits until all have (they have long since),
+// then stores E + 1 and zeroes the shards for the next launch.  The launch whose tag is 2^32 - 1 ends
+// with a fan-in whose last workgroup zeroes the hand-off region and the epoch (tags never repeat
+// over a granule's lifetime).  Bounded: a wait that does not end within ~1 s sets the error word and
+// goes on (results undefined, never a hang); with the error word set later waits return at once.
+constexpr int FQ_CHAIN_MAX = 8;
+constexpr size_t FQ_CHAIN_SYNC_BYTES = 4096;       // chain workspace: sync words, then the hand-offs
+constexpr int FQ_CHAIN_EPOCH = 8, FQ_CHAIN_ERR = 9, FQ_CHAIN_DONE = 10;  // sync words, 128 B apart;
+                                                                           // 0..7: the start counter
+__device__ __forceinline__ uint32_t chain_tag(uint32_t epoch) { return epoch + 1u; }
+
+// the caller's output pair (plain 4-byte store) and, for a linear the next one reads, its granule
+__device__ __forceinline__ void chain_store2(uint16_t *__restrict__ d, uint64_t *__restrict__ hd, uint32_t tag, int N,
+                                             int row, int col, float v0, float v1) {
+    const uint32_t pk = (uint32_t)f2h(v0) | ((uint32_t)f2h(v1) << 16);
+    const long f = (long)row * N + col;
+    *reinterpret_cast<uint32_t *>(d + f) = pk;
+    if (hd) __hip_atomic_store(hd + (f >> 1), ((uint64_t)tag << 32) | pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// workgroup 0, linear 1: every workgroup has read the epoch -> advance it, zero the start counter
+__device__ __forceinline__ void chain_epoch(uint32_t *__restrict__ sync, uint32_t epoch, int grid, int wid) {
+    if (wid == 0) {
+        const int lane = threadIdx.x & 63;
+        uint32_t *err = sync + 32 * FQ_CHAIN_ERR;
+        const uint32_t target = lane < 8 ? (uint32_t)((grid - lane + 7) >> 3) : 0u;
+        bool ok = lane >= 8;
+        for (int spin = 0; spin < (1 << 20); spin++) {
+            if (!ok) ok = __hip_atomic_load(sync + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (lane < 8) {
+            __hip_atomic_store(sync + 32 * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __builtin_amdgcn_s_barrier();
+}
+
 // ---- deferred split-K fix-up of the decode kernels.  Every item's partial tile went out as
 // write-through (sc1) slab stores; one drain, then one agent-scope ticket per item (taken in
 // parallel, one lane each), and the last arriver of a tile sums its S slabs in z order.
@@ -284,7 +341,8 @@ __device__ __forceinline__ void dequant4(float (&c)[4], v4i acc, __half2 p01, __
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
-template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0, bool GAT = false>
+template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0, bool GAT = false,
+          bool CHN = false>
 __device__ __forceinline__ void decode_body(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
@@ -307,6 +365,7 @@ __device__ __forceinline__ void decode_body(
     constexpr int NW = decode_waves(MT), D = C::D, RG = C::RG, XSR = C::XSR;
     static_assert(!FUSE || (XS == 0 && SS == 0), "fused quantization stages into LDS");
     static_assert(PRO == 0 || (FUSE && !CH), "fused producers run in the fused quantizer's prologue");
+    static_assert(!CHN || (FUSE && PRO == 0 && !GAT && !CH && !DBG), "the chain runs plain fused linears");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FQ_STAMP(0);
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
@@ -563,7 +622,7 @@ __device__ __forceinline__ void decode_body(
     // the peer-store gather kernel whose x is the previous gather's output: its wait is folded in
     // here (gather_poll), after the ring is issued; the activation window follows the poll
     const bool wfold = GAT && FUSE && pro.wgat != nullptr;
-    if (FUSE && n > 0 && !wfold) x_fetch(0);
+    if (FUSE && n > 0 && !wfold && !CHN) x_fetch(0);
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
     auto advance = [&]() {
         if (++rj == ng) {
@@ -587,8 +646,59 @@ __device__ __forceinline__ void decode_body(
         gather_poll(pro.wgat, pro.werr, wid);
         if (n > 0) x_fetch(0);
     }
+    if (CHN && pro.link == 1 && blockIdx.x == 0 && pro.epoch != 0xfffffffeu) chain_epoch(pro.chain, pro.epoch, gridall, wid);
 
-    if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
+    if (CHN && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers
+        // lane (pair c + 4u + lane / 16, chunk lane % 16): 8 fp16 values; from the hand-off, its four
+        // granules (32 B), re-loaded until every tag is this launch's tag of the previous linear
+        const bool gr = pro.hx != nullptr;
+        const uint32_t want = chain_tag(pro.epoch);
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+            gr ? (void *)pro.hx : (void *)xh, (short)0, (int)((uint32_t)M * K * (gr ? 4 : 2)), 0x00020000);
+        uint32_t *err = pro.chain + 32 * FQ_CHAIN_ERR;
+        bool failed = gr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        for (int c = 0; c < R; c += 16) {  // wave-uniform
+            uint4 v[4];
+            uint32_t off[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                int rg = c + 4 * u + (lane >> 4);
+                rg = rg < R ? rg : R - 1;
+                const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+                off[u] = ((uint32_t)row * K + (uint32_t)(ga + j) * FQ_GROUP + qsub * 8) * (gr ? 4 : 2);
+            }
+            if (!gr) {
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (c + 4 * u < R) v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u], 0, 16));
+            } else {
+                for (int spin = 0; spin < (1 << 20); spin++) {
+                    bool ok = true;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (c + 4 * u >= R) break;
+                        const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u], 0, 16));
+                        const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u] + 16, 0, 16));
+                        v[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
+                        ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (spin == (1 << 20) - 1) {
+                        failed = true;
+                        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (c + 4 * u >= R) break;
+                uint2 codes;
+                const uint16_t sh = quant_group16(v[u], abits, codes);
+                x_store(c + 4 * u + (lane >> 4), codes, sh);
+            }
+        }
+    } else if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
         if (GAT && wfold)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the window was issued after the ring)
         else
@@ -812,7 +922,7 @@ __device__ __forceinline__ void decode_body(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
-            if (GAT && S == 1) {  // peer-store gather: two adjacent columns per thread
+            if ((GAT || CHN) && S == 1) {  // peer-store gather / chain: two adjacent columns per thread
                 for (int e = 2 * threadIdx.x; e < (rs + 1) * EM; e += 2 * NW * 64) {
                     const int k = e / EM, ee = e - k * EM;
                     float v0 = 0.f, v1 = 0.f;
@@ -821,7 +931,11 @@ __device__ __forceinline__ void decode_body(
                         v0 += red[(k * NW + w) * EM + ee];
                         v1 += red[(k * NW + w) * EM + ee + 1];
                     }
-                    gather_store2(gat, gat->P, ee >> 4, 16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
+                    if (CHN)
+                        chain_store2(d, pro.hd, chain_tag(pro.epoch), N, ee >> 4,
+                                     16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
+                    else
+                        gather_store2(gat, gat->P, ee >> 4, 16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
                 }
             } else
             for (int e = threadIdx.x; e < (rs + 1) * EM; e += NW * 64) {
@@ -844,6 +958,11 @@ __device__ __forceinline__ void decode_body(
         }
     }
     FQ_STAMP(3);
+    if constexpr (CHN) {  // (S = 1) the next linear's prologue reuses the LDS: every wave is past this one's
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        return;
+    }
     // GAT is a separate instantiation: the gather's branches and publish step cost the plain
     // kernel ~3.5 % per launch when they are only runtime-dead (A/B over round 3's builds,
     // tools/ab_bisect.sh)
@@ -958,6 +1077,71 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ln_kerne
     decode_body<MT, 0, 0, true, false, 0, false, 4, false>(
         nullptr, nullptr, xh, abits, wpk, Mall, N, K, d, nullptr, reinterpret_cast<float *>(ws + FQ_TICKET_BYTES),
         reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, IPW - (ir != 0), ir, 1, nullptr, pro, grid);
+}
+
+// The decode chain's kernel: the links' packed fields (decode_pack) by value in the kernel
+// arguments (40 B per linear, read by scalar loads as each linear starts); every linear runs the
+// fused plan fq_linear_w6ax would run for it (S = 1, the same grid), so the bits are the same.
+struct ChainLink {
+    const uint16_t *x;
+    const uint32_t *w;
+    uint16_t *d;
+    const uint64_t *hx;  // x's granules (the previous link's hand-off + offset), or null: x is ready
+    uint64_t *hd;        // this link's hand-off granules, or null (the last link)
+    uint32_t w0, w1, w2, w3;
+};
+struct ChainArgs {
+    ChainLink l[FQ_CHAIN_MAX];
+    uint32_t *sync;  // the chain workspace: sync words, then (hand, hand + hand_bytes) the hand-offs
+    uint4 *hand;
+    uint32_t hand_bytes;
+    int n;
+};
+template <int MT>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_kernel(const ChainArgs a) {
+    // the launch's epoch, then this workgroup's arrival on the start counter (after the load landed)
+    const uint32_t epoch = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(a.sync + 32 * FQ_CHAIN_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    uint32_t started = 0;  // (returned; waited for only in the wrapping launch)
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"s"(epoch) : "memory");
+        started = __hip_atomic_fetch_add(a.sync + 32 * (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int l = 0; l < a.n; l++) {
+        const ChainLink L = a.l[l];
+        const int N = L.w0 & 0x1fffff, abits = (L.w0 >> 21) & 15, xwin = L.w0 >> 25;
+        const int K = (L.w1 & 0x1fff) * FQ_GROUP;
+        const int IPW = L.w2 & 0xffff, RC = L.w2 >> 16;
+        const int Mall = L.w3 & 1023, ir = (L.w3 >> 10) & 2047, grid = L.w3 >> 21;
+        DecodePro pro{};
+        pro.chain = a.sync;
+        pro.link = l;
+        pro.epoch = epoch;
+        pro.hx = L.hx;
+        pro.hd = L.hd;
+        decode_body<MT, 0, 0, true, false, 0, false, 0, false, true>(
+            nullptr, nullptr, L.x, abits, L.w, Mall, N, K, L.d, nullptr, nullptr, nullptr, 1, IPW, RC, xwin,
+            IPW - (ir != 0), ir, 1, nullptr, pro, grid);
+    }
+    if (epoch == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch alone):
+        __syncthreads();         // the last workgroup to arrive clears every granule (all the others
+        __shared__ uint32_t last;  // are done reading), the start counter and the epoch
+        if (threadIdx.x == 0) {
+            asm volatile("" ::"v"(started));  // this workgroup's start arrival has been performed
+            last = __hip_atomic_fetch_add(a.sync + 32 * FQ_CHAIN_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last) {
+            for (uint32_t i = threadIdx.x; i < a.hand_bytes / 16; i += blockDim.x) a.hand[i] = make_uint4(0, 0, 0, 0);
+            if (threadIdx.x < 8)
+                __hip_atomic_store(a.sync + 32 * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x == 0) {
+                __hip_atomic_store(a.sync + 32 * FQ_CHAIN_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.sync + 32 * FQ_CHAIN_EPOCH, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 }
 
 // Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q
@@ -1992,6 +2176,124 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
     *launched = true;
     return acc_dbg ? dispatch_decode<true, true>(p, a, s) : dispatch_decode<true, false>(p, a, s);
 }
+
+// ---- decode chain: the links that can run in one persistent launch are those whose fused plan
+// is one 4-row tile set over the whole chip with no k-split (every LLaMA / OPT decode shape at
+// M <= 4 with N >= 16 x CUs), outputs in 16-column multiples, 16-byte aligned activations.
+static bool chain_plan(int M, const fq_chain_link &L, DecodePlan *p) {
+    if (M > 4 || L.N % 16 || ((uintptr_t)L.x & 15) || ((uintptr_t)L.d & 3)) return false;
+    *p = decode_plan(M, L.N, L.K, true);
+    return p->fits && p->MT == 4 && p->S == 1 && p->NCH == 1 && p->grid == device_cus() &&
+           (size_t)p->NT * (L.K / FQ_GROUP) * FQ_BLOCK < ((size_t)1 << 32);
+}
+static size_t chain_handoff_bytes(int M, int N) { return ((size_t)M * N * 4 + 255) & ~(size_t)255; }
+static bool in_range(const void *a, size_t na, const void *b, size_t nb) {  // [a, a+na) inside [b, b+nb)
+    return (uintptr_t)a >= (uintptr_t)b && (uintptr_t)a + na <= (uintptr_t)b + nb;
+}
+static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+    return (uintptr_t)a < (uintptr_t)b + nb && (uintptr_t)b < (uintptr_t)a + na;
+}
+
+extern "C" size_t fq_chain_workspace_bytes(const fq_chain_link *links, int n, int M) {
+    size_t b = FQ_CHAIN_SYNC_BYTES;
+    for (int l = 0; links && l + 1 < n; l++) b += chain_handoff_bytes(M, links[l].N);
+    return b;
+}
+
+extern "C" fq_status fq_chain_workspace_init(void *chain_ws, size_t bytes, fq_stream_t stream) {
+    if (!bytes) return FQ_OK;
+    if (!chain_ws) return FQ_ERR_NULL;
+    return hipMemsetAsync(chain_ws, 0, bytes, (hipStream_t)stream) == hipSuccess ? FQ_OK : FQ_ERR_HIP;
+}
+
+extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int M, void *chain_ws,
+                                          size_t chain_ws_bytes, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
+                                          size_t workspace_bytes, fq_stream_t stream) {
+    if (!links || n <= 0) return FQ_ERR_NULL;
+    if (M <= 0 || M > 32) return FQ_ERR_SHAPE;
+    for (int l = 0; l < n; l++) {
+        const fq_chain_link &L = links[l];
+        if (!L.x || !L.w_packed || !L.d) return FQ_ERR_NULL;
+        if (L.N <= 0 || L.K <= 0 || L.K % FQ_GROUP) return FQ_ERR_SHAPE;
+        if (L.abits != 6 && L.abits != 8) return FQ_ERR_BITS;
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    const bool ws_ok = chain_ws && chain_ws_bytes >= FQ_CHAIN_SYNC_BYTES && ((uintptr_t)chain_ws & 255) == 0;
+    char *hand = (char *)chain_ws + FQ_CHAIN_SYNC_BYTES;  // the hand-off granules of a run, link after link
+    const size_t hand_bytes = ws_ok ? (chain_ws_bytes - FQ_CHAIN_SYNC_BYTES) / 16 * 16 : 0;
+    if (hand_bytes >= ((size_t)1 << 32)) return FQ_ERR_WORKSPACE;
+    int l = 0;
+    while (l < n) {
+        // the longest run from l (at most FQ_CHAIN_MAX links) in which every link is chainable, the
+        // outputs are disjoint, and each link's x either lies inside the previous link's output (read
+        // from its hand-off granules) or overlaps no output of the run (ready before the launch)
+        DecodePlan plans[FQ_CHAIN_MAX];
+        const uint64_t *hx[FQ_CHAIN_MAX] = {};
+        int r = 0;
+        size_t used = 0;
+        while (ws_ok && l + r < n && r < FQ_CHAIN_MAX && chain_plan(M, links[l + r], &plans[r])) {
+            const fq_chain_link &L = links[l + r];
+            const size_t xb = (size_t)M * L.K * 2, db = (size_t)M * L.N * 2;
+            bool ok = true, inside = false;
+            if (r > 0) {
+                const fq_chain_link &P = links[l + r - 1];
+                inside = in_range(L.x, xb, P.d, (size_t)M * P.N * 2) && (((uintptr_t)L.x - (uintptr_t)P.d) & 3) == 0;
+                if (inside && used + chain_handoff_bytes(M, P.N) > hand_bytes) ok = false;
+            }
+            for (int i = 0; ok && i <= r; i++) {
+                const fq_chain_link &Q = links[l + i];
+                const size_t qb = (size_t)M * Q.N * 2;
+                if (i < r && ranges_overlap(L.d, db, Q.d, qb)) ok = false;      // disjoint outputs
+                if (i < r && ranges_overlap(Q.x, (size_t)M * Q.K * 2, L.d, db)) ok = false;  // no earlier x
+                if (!(inside && i == r - 1) && ranges_overlap(L.x, xb, Q.d, qb)) ok = false;  // x: hand-off or ready
+            }
+            if (!ok) break;
+            if (inside) {
+                hx[r] = reinterpret_cast<const uint64_t *>(hand + used) + ((uintptr_t)L.x - (uintptr_t)links[l + r - 1].d) / 4;
+                used += chain_handoff_bytes(M, links[l + r - 1].N);
+            }
+            r++;
+        }
+        if (r < 2) {  // a run of one is a plain linear
+            const fq_chain_link &L = links[l];
+            const fq_status st = fq_linear_w6ax(L.x, M, L.N, L.K, L.abits, L.w_packed, L.d, xq_buf, xs_buf, workspace,
+                                                workspace_bytes, stream);
+            if (st != FQ_OK) return st;
+            l++;
+            continue;
+        }
+        ChainArgs a{};
+        size_t lds = 0, off = 0;
+        for (int i = 0; i < r; i++) {
+            const fq_chain_link &L = links[l + i];
+            const DecodePlan &p = plans[i];
+            DecodePacked pk;
+            const int items = p.NT;
+            if (items / p.grid != p.IPW - (items % p.grid != 0) ||
+                !decode_pack(L.N, L.K, L.abits, p.xwin, 1, 1, p.IPW, p.RC, M, items % p.grid, p.grid, &pk))
+                return FQ_ERR_SHAPE;
+            // a link's hand-off exists when the next link reads it; the granule offsets assigned above
+            uint64_t *hd = nullptr;
+            if (i + 1 < r && hx[i + 1]) {
+                hd = reinterpret_cast<uint64_t *>(hand + off);
+                off += chain_handoff_bytes(M, L.N);
+            }
+            a.l[i] = ChainLink{L.x, (const uint32_t *)L.w_packed, L.d, hx[i], hd, pk.w0, pk.w1, pk.w2, pk.w3};
+            const size_t b = decode_lds_bytes(p, M, L.N, L.K);
+            lds = b > lds ? b : lds;
+        }
+        a.n = r;
+        a.sync = (uint32_t *)chain_ws;
+        a.hand = (uint4 *)hand;
+        a.hand_bytes = (uint32_t)hand_bytes;
+        hipLaunchKernelGGL((fq_gemm_decode_chain_kernel<4>), dim3(plans[0].grid), dim3(decode_waves(4) * 64), lds, s, a);
+        FQ_LAUNCH_CHECK();
+        l += r;
+    }
+    return FQ_OK;
+}
+
+extern "C" size_t fq_chain_error_offset(void) { return 4 * 32 * FQ_CHAIN_ERR; }
 
 // A producer fused into the one-launch decode linear (DecodePro): pro = 1, residual add + RMSNorm
 // (xh = the residual; M = 1, K = 4 * 128 * waves, no k-split), pro = 2, SiLU(xh) * in (M <= 32).

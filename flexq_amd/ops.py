@@ -78,9 +78,32 @@ def workspace(device, nbytes, stream_handle):
     return buf
 
 
+_CWS = {}  # (device, stream) -> chain workspace (fq_chain_workspace_init; written by chain launches only)
+
+
+def chain_workspace(device, nbytes, stream_handle):
+    """Per-(device, stream) chain workspace of fq_linear_chain_w6ax: zeroed once, then written by chain
+    launches only; grown like workspace() (a superseded one a capture has seen is kept)."""
+    key = (device, stream_handle)
+    buf = _CWS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        old = buf.numel() if buf is not None else 0
+        nbytes = max(nbytes, old + old // 2, 1 << 20)
+        nbytes = (nbytes + (1 << 20) - 1) >> 20 << 20
+        if buf is not None and id(buf) in _WS_CAPTURED:
+            _WS_RETIRED.append(buf)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _lib.call("fq_chain_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
+        _CWS[key] = buf
+    if torch.cuda.is_current_stream_capturing():
+        _WS_CAPTURED.add(id(buf))
+    return buf
+
+
 def workspace_device_bytes():
     """Bytes held by the workspaces (current and retired), for tests and diagnostics."""
-    return sum(b.numel() for b in _WS.values()) + sum(b.numel() for b in _WS_RETIRED)
+    return (sum(b.numel() for b in _WS.values()) + sum(b.numel() for b in _CWS.values()) +
+            sum(b.numel() for b in _WS_RETIRED))
 
 
 def reserve_workspace(device, shapes, stream=None):
@@ -230,6 +253,66 @@ def linear_w6ax(x, wpk, N, abits=6, out=None, w_u8=None):
     _lib.call("fq_linear_w6ax", _ptr(x), M, N, K, abits, _ptr(wpk), _ptr(out), _ptr(xq),
               _ptr(xs), _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
     return out
+
+
+class _ChainLink(ctypes.Structure):  # fq_chain_link (include/flexq_hip.h)
+    _fields_ = [("x", ctypes.c_void_p), ("w_packed", ctypes.c_void_p), ("d", ctypes.c_void_p),
+                ("N", ctypes.c_int), ("K", ctypes.c_int), ("abits", ctypes.c_int)]
+
+
+def linear_chain_w6ax(links):
+    """Consecutive decode linears (fq_linear_chain_w6ax): links = [(x, wpk, N, abits, out), ...], each
+    computed exactly as linear_w6ax(x, wpk, N, abits, out=out), in order; x may be a view of an
+    earlier link's out (the chain's dependency).  Runs of chainable links (M <= 4) are
+    one persistent launch each.  Returns the list of outputs."""
+    _need(len(links) > 0, "empty chain")
+    M = None
+    arr = (_ChainLink * len(links))()
+    scratch = 0
+    for i, (x, wpk, N, abits, out) in enumerate(links):
+        _dev(x, torch.float16, "x", 2)
+        m, K = x.shape
+        _need(x.stride(1) == 1 and x.stride(0) == K, "x must be a contiguous [M, K] row block")
+        M = m if M is None else M
+        _need(m == M, "every link has the same M")
+        _k_ok(K)
+        _img_ok(wpk, N, K)
+        _need(abits in (6, 8), "abits must be 6 or 8")
+        _dev(out, torch.float16, "out", 2)
+        _need(tuple(out.shape) == (M, N), f"out must be [M, N] = {(M, N)}")
+        _need(wpk.device == x.device == out.device == links[0][0].device, "one device")
+        _need(not _overlap(out, x), "a link's output must not overlap its input")
+        arr[i] = _ChainLink(_ptr(x), _ptr(wpk), _ptr(out), N, K, abits)
+        scratch = max(scratch, act_scratch_bytes(M, N, K) and M * K)
+    dev = links[0][0].device
+    xq = xs = None
+    if scratch:
+        Kmax = max(x.shape[1] for (x, *_r) in links)
+        xq = torch.empty((M, Kmax), dtype=torch.int8, device=dev)
+        xs = torch.empty((Kmax // GROUP, M), dtype=torch.float16, device=dev)
+    s = _stream(links[0][0])
+    cb = int(_lib.load().fq_chain_workspace_bytes(ctypes.cast(arr, ctypes.c_void_p), len(links), M))
+    cbuf = chain_workspace(dev, cb, s.value)
+    nb = max(gemm_workspace_bytes(M, N, x.shape[1]) for (x, _w, N, _a, _o) in links)
+    wbuf = workspace(dev, nb, s.value)
+    _lib.call("fq_linear_chain_w6ax", ctypes.cast(arr, ctypes.c_void_p), len(links), M, _ptr(cbuf),
+              ctypes.c_size_t(cbuf.numel()), _ptr(xq), _ptr(xs), _ptr(wbuf),
+              ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return [l[4] for l in links]
+
+
+def chain_error(device=None, stream=None):
+    """The decode chain's sticky error word in the stream's chain workspace (0: every in-kernel wait
+    ended in time; 1: one timed out and the results since are undefined)."""
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    buf = _CWS.get((dev, s.cuda_stream))
+    if buf is None:
+        return 0
+    off = int(_lib.load().fq_chain_error_offset())
+    return int(buf[off:off + 4].view(torch.int32).item())
 
 
 def act_scratch_bytes(M, N, K):

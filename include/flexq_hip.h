@@ -125,6 +125,35 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
                          uint16_t *d, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                          size_t workspace_bytes, fq_stream_t stream);
 
+/* ---- decode chain ------------------------------------------------------------------------------
+ * n consecutive linears, each computed as fq_linear_w6ax(links[l].x, M, N, K, abits, w_packed, d, ...)
+ * in order -- bit-identical outputs -- where links[l].x may lie inside links[l-1].d (a layer's o_proj ->
+ * gate_up -> down -> next qkv).  Runs of up to 8 links run as ONE persistent launch when every link's
+ * decode plan allows it (M <= 4, N a multiple of 16 and >= 16 x the CU count, x 16-byte aligned) and
+ * the run's outputs are disjoint and each x lies either inside the previous link's d (4-byte offset)
+ * or outside every output of the run: each linear's weight stream starts before it waits, inside the
+ * kernel, for the previous linear's output (read from tagged hand-off granules in the workspace), not
+ * behind a kernel boundary.  Other links run as fq_linear_w6ax (xq_buf / xs_buf as
+ * there: only links that do not fuse their quantizer use them; workspace as fq_linear_w6ax's).
+ * chain_ws: the chain workspace, 256-byte aligned, fq_chain_workspace_bytes(links, n, M) bytes (a
+ * shorter one runs shorter runs or plain linears), zeroed once by fq_chain_workspace_init and then
+ * written by chain launches only (one per stream; it may serve every chain of that stream).
+ * A chain launch never hangs: a wait that does not end within ~1 s sets the word at byte offset
+ * fq_chain_error_offset() of chain_ws (sticky; results undefined) -- the caller checks it.
+ * No FlexQ counterpart: the reference launches one kernel per GEMM call (flexq_gemm_wrapper.cu:99-122). */
+typedef struct fq_chain_link {
+    const uint16_t *x;    /* fp16 [M][K] */
+    const void *w_packed; /* weight image [N][K] */
+    uint16_t *d;          /* fp16 [M][N] */
+    int N, K, abits;
+} fq_chain_link;
+fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int M, void *chain_ws, size_t chain_ws_bytes,
+                               int8_t *xq_buf, uint16_t *xs_buf, void *workspace, size_t workspace_bytes,
+                               fq_stream_t stream);
+size_t fq_chain_workspace_bytes(const fq_chain_link *links, int n, int M);
+fq_status fq_chain_workspace_init(void *chain_ws, size_t bytes, fq_stream_t stream);
+size_t fq_chain_error_offset(void);
+
 /* ---- prefill with resident unpacked weights ------------------------------------------------------
  * At M >= 2048 fq_gemm_w6ax unpacks the weight image into int8 MFMA operands in its workspace on
  * every call (fq_unpack_w8_kernel: 0.75 B read + 1 B written per weight).  A caller that keeps the

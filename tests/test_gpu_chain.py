@@ -1,0 +1,168 @@
+"""The decode chain (fq_linear_chain_w6ax): consecutive dependent linears in one persistent launch,
+each waiting in the kernel for the previous linear's output.  Every output must be bit-identical to
+running the same linears one fq_linear_w6ax launch at a time, over chains of a LLaMA-2-7B layer
+(o -> gate_up -> down (A8) -> next qkv, each input the leading M*K values of the previous output, as
+bench.py's step), uneven per-link load (LLaMA-2-70B shapes beside 7B ones), runs split at 8 links,
+links that cannot chain (k-split shapes, M > 4) interleaved, repeated launches and graph replays (the
+hand-off tags advance with the epoch, the start counter returns to zero, the wrap of the tag clears
+the hand-off region), and the error word stays 0 throughout."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from flexq_amd import ops as _ops
+    return _ops
+
+
+def image(ops, N, K, g, dev):
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    ws = ((torch.rand((K // 128, N), device=dev, generator=g) + 0.5) / (18.5 * 1.04 * K ** 0.5)).half()
+    return ops.pack_w6(wq, ws)
+
+
+LAYER_7B = [(4096, 4096, 6), (22016, 4096, 6), (4096, 11008, 8), (12288, 4096, 6)]
+
+
+def build(ops, dev, M, shapes, seed=5):
+    """links [(x, wpk, N, abits, out)] where x of link l is the leading M*K of link l-1's output."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x0 = torch.randn((M, shapes[0][1]), dtype=torch.float16, device=dev, generator=g)
+    links, prev = [], x0
+    for (N, K, abits) in shapes:
+        x = prev.view(-1)[:M * K].view(M, K) if prev is not x0 else x0
+        out = torch.full((M, N), float("nan"), dtype=torch.float16, device=dev)
+        links.append((x, image(ops, N, K, g, dev), N, abits, out))
+        prev = out
+    return links
+
+
+def sequential(ops, links, dev):
+    """The same linears one launch at a time, into fresh buffers (inputs re-pointed at them)."""
+    outs, prev_src, prev_dst = [], None, None
+    for (x, wpk, N, abits, out) in links:
+        M, K = x.shape
+        if prev_src is not None and x.data_ptr() >= prev_src.data_ptr() and \
+                x.data_ptr() < prev_src.data_ptr() + prev_src.numel() * 2:
+            off = (x.data_ptr() - prev_src.data_ptr()) // 2
+            xs = prev_dst.view(-1)[off:off + M * K].view(M, K)
+        else:
+            xs = x
+        y = ops.linear_w6ax(xs, wpk, N, abits)
+        outs.append(y)
+        prev_src, prev_dst = out, y
+    torch.cuda.synchronize()
+    return outs
+
+
+def check(ops, links, dev, what):
+    ref = sequential(ops, links, dev)
+    for i, ((*_, out), r) in enumerate(zip(links, ref)):
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), r.cpu().numpy().view(np.uint16),
+                                      err_msg=f"{what}: link {i}")
+    assert ops.chain_error(dev) == 0, f"{what}: a chain wait timed out"
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+def test_chain_layer_bit_identical(ops, dev, M):
+    links = build(ops, dev, M, LAYER_7B + LAYER_7B[:3])  # two layers' worth: 7 links, one launch
+    for rep in range(3):  # repeated launches: the counters are zero again after each
+        for (*_, out) in links:
+            out.fill_(float("nan"))
+        ops.linear_chain_w6ax(links)
+        torch.cuda.synchronize()
+        check(ops, links, dev, f"M={M} rep {rep}")
+
+
+def test_chain_uneven_links_and_run_split(ops, dev):
+    """70B gate_up (7 tiles per CU) beside 1-tile links, 11 links: runs of 8 and 3."""
+    shapes = [(28672, 8192, 6), (8192, 28672, 8), (4096, 8192, 6), (8192, 4096, 6), (57344, 8192, 6),
+              (8192, 28672, 8), (4096, 8192, 6), (12288, 4096, 6), (4096, 4096, 6), (22016, 4096, 6),
+              (4096, 11008, 8)]
+    links = build(ops, dev, 1, shapes, seed=9)
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    check(ops, links, dev, "uneven")
+
+
+def test_chain_with_unchainable_links(ops, dev):
+    """Links whose plan is not one S = 1 tile set over the chip (N = 1024: k-split; N = 2000 not a
+    multiple of 16) run as plain linears between chained runs; same bits."""
+    shapes = [(4096, 4096, 6), (1024, 4096, 6), (4096, 1024, 8), (12288, 4096, 6), (2000, 4096, 6),
+              (4096, 1024, 6), (11008, 4096, 6), (4096, 11008, 8)]
+    links = build(ops, dev, 1, shapes, seed=3)
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    check(ops, links, dev, "mixed")
+
+
+def test_chain_m16_falls_back(ops, dev):
+    """M > 4: every link runs as fq_linear_w6ax (quantize launches included); same bits."""
+    links = build(ops, dev, 16, LAYER_7B, seed=4)
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    check(ops, links, dev, "M=16")
+
+
+def test_chain_graph_replay(ops, dev):
+    links = build(ops, dev, 1, LAYER_7B * 2, seed=6)
+    s = torch.cuda.Stream(dev)
+    ops.reserve_workspace(dev, [(1, 22016, 4096)], stream=s)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        ops.linear_chain_w6ax(links)  # warm-up on the capture stream
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        ops.linear_chain_w6ax(links)
+    for rep in range(5):
+        for (*_, out) in links:
+            out.fill_(float("nan"))
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            g.replay()
+        s.synchronize()
+        ref = sequential(ops, links, dev)
+        for i, ((*_, out), r) in enumerate(zip(links, ref)):
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), r.cpu().numpy().view(np.uint16),
+                                          err_msg=f"replay {rep} link {i}")
+    assert ops.chain_error(dev, stream=s) == 0
+
+
+def test_chain_rejections(ops, dev):
+    links = build(ops, dev, 1, LAYER_7B[:2], seed=2)
+    x, wpk, N, abits, out = links[0]
+    with pytest.raises(ValueError):
+        ops.linear_chain_w6ax([(x, wpk, N, abits, x.view(-1)[:N].view(1, N))])  # output over its input
+    with pytest.raises(ValueError):
+        ops.linear_chain_w6ax([links[0], (torch.zeros((2, 4096), dtype=torch.float16, device=dev),) + links[1][1:]])
+
+
+def test_chain_sync_words_and_epoch_wrap(ops, dev):
+    """After every chain launch the start counter is zero and the epoch has advanced by one; the
+    launch whose tag is 2^32 - 1 clears the hand-off granules and the epoch (tags never repeat)."""
+    links = build(ops, dev, 1, LAYER_7B, seed=8)
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    buf = ops._CWS[(links[0][0].device, torch.cuda.current_stream(dev).cuda_stream)]
+    words = buf[:4096].view(torch.int32)  # sync words 128 B apart: 0..7 start counter, 8 epoch, 9 error
+    e0 = int(words[8 * 32].item())
+    assert e0 >= 1 and all(int(words[32 * s].item()) == 0 for s in range(8))
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    assert int(words[8 * 32].item()) == e0 + 1
+    words[8 * 32] = -2  # the next launch's tag is 0xffffffff
+    for rep, want in ((0, 0), (1, 1), (2, 2)):
+        for (*_, out) in links:
+            out.fill_(float("nan"))
+        ops.linear_chain_w6ax(links)
+        torch.cuda.synchronize()
+        check(ops, links, dev, f"wrap rep {rep}")
+        assert int(words[8 * 32].item()) == want
+        assert all(int(words[32 * s].item()) == 0 for s in range(8)) and int(words[10 * 32].item()) == 0
+    tags = buf[4096:].view(torch.int32)[1::2]  # every granule's tag word
+    assert bool(((tags >= 0) & (tags <= 2)).all().item())  # no tag older than the wrap survives
