@@ -178,6 +178,25 @@ def run_step(stack, M, world, group=None, gather=True, staged=False):
                 dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
 
 
+def chain_runs(stack):
+    """The step's linears as decode chains (fq_linear_chain_w6ax), cut where the model's attention core
+    sits: qkv_0 | o_0, gate_up_0, down_0, qkv_1 | o_1, ... -- the attention (out of scope) is a kernel of
+    its own between qkv and o, so a chain never spans it; each chain is one persistent launch."""
+    runs, cur = [], []
+    for name, p in linears(stack):
+        if name == "o" and cur:
+            runs.append(cur)
+            cur = []
+        cur.append((p["x"], p["pk"], p["Nl"], p["abits"], p["out"]))
+    runs.append(cur)
+    return runs
+
+
+def run_chains(runs):
+    for r in runs:
+        ops.linear_chain_w6ax(r)
+
+
 def capture(fn, stream):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=stream):
@@ -801,6 +820,9 @@ def main():
                     help="N = 1: skip the reference's kernel sweep (engine/test_flexq_kernel.sh, README.md:189's form)")
     ap.add_argument("--no-layers", action="store_true",
                     help="skip the end-to-end decoder-layer comparison against fp16 (M = 1 and 16)")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="N = 1 decode: time only one launch per linear (default: also the decode chains, "
+                         "fq_linear_chain_w6ax, taken for `value` when bit-identical and faster)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo with host-staged gathers, no graph")
     a = ap.parse_args()
@@ -837,6 +859,7 @@ def main():
     n_lin = layers * len(launch_lins)
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)  # whole model, counted once
 
+    decode_form, chain_sec = "one fq_linear_w6ax launch per linear", None
     if tp > 1:
         r = measure_tp(ctx, hcfg, merge, tp, a.steps, a.warmup)
         # The column-parallel step's all-gather has two implementations: RCCL's all_gather and the
@@ -867,6 +890,28 @@ def main():
         use_graph = not a.no_graph
         replay = ctx.prepare(lambda: run_step(stack, M, 1), use_graph)
         elapsed, ev_s = ctx.timed(replay, a.steps, a.warmup)
+        if M <= 4 and not prefill and not a.no_chain:
+            # the same step as decode chains: one persistent launch per run of linears between attention
+            # cores, each linear waiting in-kernel for its input; taken for `value` only
+            # when the step's output is bit-identical, no in-kernel wait timed out, and it is faster
+            last_out = linears(stack)[-1][1]["out"]
+            ref_bits = last_out.cpu().numpy().view(np.uint16).copy()
+            runs = chain_runs(stack)
+            replay_c = ctx.prepare(lambda: run_chains(runs), use_graph)
+            el_c, ev_c = ctx.timed(replay_c, a.steps, a.warmup)
+            same = bool(np.array_equal(last_out.cpu().numpy().view(np.uint16), ref_bits))
+            err = ops.chain_error(dev, stream=ctx.stream)
+            chain_sec = {"what": "the same step as decode chains (fq_linear_chain_w6ax): qkv_0 | o_i, gate_up_i, "
+                                 "down_i, qkv_i+1 | ... -- one persistent launch per run between attention cores, "
+                                 "each linear's weight stream issued before it waits in-kernel for its input "
+                                 "(tagged hand-off granules)",
+                         "launches_per_step": len(runs), "ms_per_step": round(el_c / a.steps * 1e3, 4),
+                         "launches_ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                         "bit_identical_to_launches": same, "wait_timed_out": bool(err)}
+            if same and not err and el_c < elapsed:
+                elapsed, ev_s = el_c, ev_c
+                decode_form = f"decode chains: {len(runs)} persistent launches per step (fq_linear_chain_w6ax)"
+            del replay_c
         replicas = world  # independent token streams (dp), each through the whole model
         value = replicas * flops_step * a.steps / elapsed / 1e12
         tok_s = replicas * M * a.steps / elapsed
@@ -924,9 +969,12 @@ def main():
                             f"dp{world}: independent replicas, one token stream per GPU, no data-path collective"),
             "graph": use_graph,
             "launches_per_layer": [[name, N // tp, K, ab] for (name, N, K, ab) in launch_lins],
+            "decode_form": decode_form if tp == 1 else "one launch per linear",
         },
         "roofline": {
-            "kernel": ("fq_gemm_decode_kernel<FUSE>" if fused_all else
+            "kernel": ("fq_gemm_decode_chain_kernel (per linear: step time / linears)" if
+                       (tp == 1 and decode_form.startswith("decode chains")) else
+                       "fq_gemm_decode_kernel<FUSE>" if fused_all else
                        "fq_gemm_decode_kernel (+ quantize where unfused)"),
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -945,6 +993,8 @@ def main():
                                        "HIP events on the capture stream; max over ranks"),
         },
     }
+    if tp == 1 and chain_sec is not None:
+        res["decode_chain"] = chain_sec
     if staged:
         res["rehearsal"] = "--share-gpu: all ranks on one GPU, gloo with host-staged gathers (not a valid result)"
     if prefill and tp == 1:

@@ -203,6 +203,12 @@ constexpr size_t FQ_CHAIN_SYNC_BYTES = 4096;       // chain workspace: sync word
 constexpr int FQ_CHAIN_EPOCH = 8, FQ_CHAIN_ERR = 9, FQ_CHAIN_DONE = 10;  // sync words, 128 B apart;
                                                                            // 0..7: the start counter
 __device__ __forceinline__ uint32_t chain_tag(uint32_t epoch) { return epoch + 1u; }
+// The epoch is loaded as the launch starts and first needed a linear later: every use goes through
+// this (volatile: not hoisted to the load), so no wave waits for it before its first DMA.
+__device__ __forceinline__ uint32_t chain_late(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 // the caller's output pair (plain 4-byte store) and, for a linear the next one reads, its granule
 __device__ __forceinline__ void chain_store2(uint16_t *__restrict__ d, uint64_t *__restrict__ hd, uint32_t tag, int N,
@@ -213,26 +219,29 @@ __device__ __forceinline__ void chain_store2(uint16_t *__restrict__ d, uint64_t 
     if (hd) __hip_atomic_store(hd + (f >> 1), ((uint64_t)tag << 32) | pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// workgroup 0, linear 1: every workgroup has read the epoch -> advance it, zero the start counter
-__device__ __forceinline__ void chain_epoch(uint32_t *__restrict__ sync, uint32_t epoch, int grid, int wid) {
-    if (wid == 0) {
-        const int lane = threadIdx.x & 63;
-        uint32_t *err = sync + 32 * FQ_CHAIN_ERR;
-        const uint32_t target = lane < 8 ? (uint32_t)((grid - lane + 7) >> 3) : 0u;
-        bool ok = lane >= 8;
-        for (int spin = 0; spin < (1 << 20); spin++) {
-            if (!ok) ok = __hip_atomic_load(sync + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
-            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
-            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (lane < 8) {
-            __hip_atomic_store(sync + 32 * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (lane == 0) __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+// Workgroup 0 advances the epoch once every workgroup has read it (each adds to the start counter
+// after its first linear, whose tag needed the epoch): wave 0 loads the counter's shards as linear 1
+// starts (chain_epoch_load, not waited for), and after linear 1's stores (chain_epoch_update) it
+// stores epoch + 1 and zeroes the shards if all had arrived -- they have, a linear earlier -- else it
+// polls for them there (bounded).
+__device__ __forceinline__ uint32_t chain_epoch_load(uint32_t *__restrict__ sync) {
+    const int lane = threadIdx.x & 63;
+    return lane < 8 ? __hip_atomic_load(sync + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+}
+__device__ __forceinline__ void chain_epoch_update(uint32_t *__restrict__ sync, uint32_t epoch, uint32_t seen, int grid) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t target = lane < 8 ? (uint32_t)((grid - lane + 7) >> 3) : 0u;
+    bool ok = seen >= target;
+    for (int spin = 0; spin < (1 << 20) && __builtin_amdgcn_ballot_w64(!ok) != 0; spin++) {
+        __builtin_amdgcn_s_sleep(2);
+        if (!ok) ok = __hip_atomic_load(sync + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
     }
-    __builtin_amdgcn_s_barrier();
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+        if (lane == 0) __hip_atomic_store(sync + 32 * FQ_CHAIN_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (lane < 8) {
+        __hip_atomic_store(sync + 32 * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // ---- deferred split-K fix-up of the decode kernels.  Every item's partial tile went out as
@@ -623,6 +632,24 @@ __device__ __forceinline__ void decode_body(
     // here (gather_poll), after the ring is issued; the activation window follows the poll
     const bool wfold = GAT && FUSE && pro.wgat != nullptr;
     if (FUSE && n > 0 && !wfold && !CHN) x_fetch(0);
+    // the chain: lane (pair c + 4u + lane / 16, chunk lane % 16) holds 8 fp16 values of x -- as 16 bytes
+    // of x itself (an input ready before the launch: gr false), or as the four 8-byte granules of the
+    // previous linear's hand-off (gr)
+    const bool gr = CHN && pro.hx != nullptr;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        gr ? (void *)pro.hx : (void *)xh, (short)0, (int)((uint32_t)M * K * (gr ? 4 : 2)), 0x00020000);
+    auto chn_off = [&](int c, int u) -> uint32_t {
+        int rg = c + 4 * u + (lane >> 4);
+        rg = rg < R ? rg : R - 1;
+        const int j = M == 1 ? rg : rg / M, row = rg - j * M;
+        return ((uint32_t)row * K + (uint32_t)(ga + j) * FQ_GROUP + qsub * 8) * (gr ? 4 : 2);
+    };
+    uint4 xv0[4];  // a ready x's first 16 pairs: loaded ahead of the ring, so they arrive first
+    if (CHN && !gr && n > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (4 * u < R) xv0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, chn_off(0, u), 0, 16));
+    }
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
     auto advance = [&]() {
         if (++rj == ng) {
@@ -646,28 +673,24 @@ __device__ __forceinline__ void decode_body(
         gather_poll(pro.wgat, pro.werr, wid);
         if (n > 0) x_fetch(0);
     }
-    if (CHN && pro.link == 1 && blockIdx.x == 0 && pro.epoch != 0xfffffffeu) chain_epoch(pro.chain, pro.epoch, gridall, wid);
+    // workgroup 0 advances the epoch around linear 1 (not in the launch whose tag wraps)
+    const bool eupd = CHN && pro.link == 1 && blockIdx.x == 0 && wid == 0 && chain_late(pro.epoch) != 0xfffffffeu;
+    const uint32_t eseen = eupd ? chain_epoch_load(pro.chain) : 0u;
 
-    if (CHN && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers
-        // lane (pair c + 4u + lane / 16, chunk lane % 16): 8 fp16 values; from the hand-off, its four
-        // granules (32 B), re-loaded until every tag is this launch's tag of the previous linear
-        const bool gr = pro.hx != nullptr;
-        const uint32_t want = chain_tag(pro.epoch);
-        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-            gr ? (void *)pro.hx : (void *)xh, (short)0, (int)((uint32_t)M * K * (gr ? 4 : 2)), 0x00020000);
+    if (CHN && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers; from the hand-off,
+        // each lane's four granules re-loaded until every tag is this launch's tag
+        const uint32_t want = gr ? chain_tag(chain_late(pro.epoch)) : 0u;
         uint32_t *err = pro.chain + 32 * FQ_CHAIN_ERR;
         bool failed = gr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
         for (int c = 0; c < R; c += 16) {  // wave-uniform
             uint4 v[4];
             uint32_t off[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                int rg = c + 4 * u + (lane >> 4);
-                rg = rg < R ? rg : R - 1;
-                const int j = M == 1 ? rg : rg / M, row = rg - j * M;
-                off[u] = ((uint32_t)row * K + (uint32_t)(ga + j) * FQ_GROUP + qsub * 8) * (gr ? 4 : 2);
-            }
-            if (!gr) {
+            for (int u = 0; u < 4; u++) off[u] = chn_off(c, u);
+            if (!gr && c == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = xv0[u];
+            } else if (!gr) {
 #pragma unroll
                 for (int u = 0; u < 4; u++)
                     if (c + 4 * u < R) v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u], 0, 16));
@@ -785,6 +808,7 @@ __device__ __forceinline__ void decode_body(
         }
     }
 
+    const uint32_t otag = CHN ? chain_tag(chain_late(pro.epoch)) : 0u;  // (the chain's output granules)
     int arow[RG];  // A-operand rows (rows >= M mirror row M-1, never stored)
 #pragma unroll
     for (int rg = 0; rg < RG; rg++) arow[rg] = 16 * rg + (lane & 15) < M ? 16 * rg + (lane & 15) : M - 1;
@@ -932,7 +956,7 @@ __device__ __forceinline__ void decode_body(
                         v1 += red[(k * NW + w) * EM + ee + 1];
                     }
                     if (CHN)
-                        chain_store2(d, pro.hd, chain_tag(pro.epoch), N, ee >> 4,
+                        chain_store2(d, pro.hd, otag, N, ee >> 4,
                                      16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
                     else
                         gather_store2(gat, gat->P, ee >> 4, 16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
@@ -958,7 +982,9 @@ __device__ __forceinline__ void decode_body(
         }
     }
     FQ_STAMP(3);
-    if constexpr (CHN) {  // (S = 1) the next linear's prologue reuses the LDS: every wave is past this one's
+    if constexpr (CHN) {  // (S = 1)
+        if (eupd) chain_epoch_update(pro.chain, chain_late(pro.epoch), eseen, gridall);
+        // the next linear's prologue reuses the LDS: every wave is past this one's
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         return;
@@ -1090,55 +1116,87 @@ struct ChainLink {
     uint64_t *hd;        // this link's hand-off granules, or null (the last link)
     uint32_t w0, w1, w2, w3;
 };
-struct ChainArgs {
-    ChainLink l[FQ_CHAIN_MAX];
-    uint32_t *sync;  // the chain workspace: sync words, then (hand, hand + hand_bytes) the hand-offs
-    uint4 *hand;
+// The sync pointer and link 0 lead the arguments as scalars (the first 48 bytes preloaded into SGPRs
+// at wave start -- an aggregate argument is not --, link 0's hand-off pointer after them: it is read
+// at the epilogue; link 0 never reads granules); the other links follow in a struct, read from
+// a copy of the whole argument block that every wave loads into VGPRs as it starts (two dwords per
+// lane, v_readlane per field): no scalar round trip before the first DMA or between linears.
+struct ChainTail {
+    ChainLink l[FQ_CHAIN_MAX - 1];  // links 1 ..
+    uint4 *hand;                    // the hand-off region (cleared when the tag wraps)
     uint32_t hand_bytes;
-    int n;
+    int n;  // >= 2
 };
+constexpr int FQ_CHAIN_TAIL_OFF = 56;  // the tail's byte offset in the arguments
+static_assert(sizeof(ChainLink) == 56 && FQ_CHAIN_TAIL_OFF + sizeof(ChainTail) <= 512,
+              "the chain's argument copy is 64 lanes x 8 bytes");
 template <int MT>
-__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_kernel(const ChainArgs a) {
-    // the launch's epoch, then this workgroup's arrival on the start counter (after the load landed)
-    const uint32_t epoch = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(a.sync + 32 * FQ_CHAIN_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+__device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLink &L, uint32_t epoch) {
+    const int N = L.w0 & 0x1fffff, abits = (L.w0 >> 21) & 15, xwin = L.w0 >> 25;
+    const int K = (L.w1 & 0x1fff) * FQ_GROUP;
+    const int IPW = L.w2 & 0xffff, RC = L.w2 >> 16;
+    const int Mall = L.w3 & 1023, ir = (L.w3 >> 10) & 2047, grid = L.w3 >> 21;
+    DecodePro pro{};
+    pro.chain = sync;
+    pro.link = l;
+    pro.epoch = epoch;
+    pro.hx = L.hx;
+    pro.hd = L.hd;
+    decode_body<MT, 0, 0, true, false, 0, false, 0, false, true>(
+        nullptr, nullptr, L.x, abits, L.w, Mall, N, K, L.d, nullptr, nullptr, nullptr, 1, IPW, RC, xwin,
+        IPW - (ir != 0), ir, 1, nullptr, pro, grid);
+}
+template <int MT>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_kernel(
+    uint32_t *__restrict__ sync, const uint16_t *x0, const uint32_t *w0p, uint16_t *d0, uint32_t p0, uint32_t p1,
+    uint32_t p2, uint32_t p3, uint64_t *hd0, const ChainTail t) {
+    const int lane = threadIdx.x & 63;
+    typedef const uint32_t __attribute__((address_space(4))) kdword;  // (the constant address space)
+    const kdword *ka = (const kdword *)__builtin_amdgcn_kernarg_segment_ptr();
+    const uint32_t dvx = ka[2 * lane], dvy = ka[2 * lane + 1];
+    // the launch's epoch (used through chain_late, a linear later)
+    const uint32_t epoch = __hip_atomic_load(sync + 32 * FQ_CHAIN_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    chain_link<MT>(sync, 0, ChainLink{x0, w0p, d0, nullptr, hd0, p0, p1, p2, p3}, epoch);
+    // this workgroup has read the epoch (its tags were stored): arrive on the start counter
     uint32_t started = 0;  // (returned; waited for only in the wrapping launch)
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"s"(epoch) : "memory");
-        started = __hip_atomic_fetch_add(a.sync + 32 * (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)
+        started = __hip_atomic_fetch_add(sync + 32 * (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto rd = [&](int k) -> uint32_t {  // dword k of the arguments (wave-uniform k)
+        return __builtin_amdgcn_readlane((k & 1) ? dvy : dvx, k >> 1);
+    };
+    auto rd64 = [&](int k) -> uint64_t { return (uint64_t)rd(k) | ((uint64_t)rd(k + 1) << 32); };
+    constexpr int T0 = FQ_CHAIN_TAIL_OFF / 4, LW = sizeof(ChainLink) / 4;
+    const int n = (int)rd(T0 + offsetof(ChainTail, n) / 4);
+    for (int l = 1; l < n; l++) {
+        const int b = T0 + (l - 1) * LW;
+        ChainLink L;
+        L.x = reinterpret_cast<const uint16_t *>(rd64(b));
+        L.w = reinterpret_cast<const uint32_t *>(rd64(b + 2));
+        L.d = reinterpret_cast<uint16_t *>(rd64(b + 4));
+        L.hx = reinterpret_cast<const uint64_t *>(rd64(b + 6));
+        L.hd = reinterpret_cast<uint64_t *>(rd64(b + 8));
+        L.w0 = rd(b + 10);
+        L.w1 = rd(b + 11);
+        L.w2 = rd(b + 12);
+        L.w3 = rd(b + 13);
+        chain_link<MT>(sync, l, L, epoch);
     }
-    for (int l = 0; l < a.n; l++) {
-        const ChainLink L = a.l[l];
-        const int N = L.w0 & 0x1fffff, abits = (L.w0 >> 21) & 15, xwin = L.w0 >> 25;
-        const int K = (L.w1 & 0x1fff) * FQ_GROUP;
-        const int IPW = L.w2 & 0xffff, RC = L.w2 >> 16;
-        const int Mall = L.w3 & 1023, ir = (L.w3 >> 10) & 2047, grid = L.w3 >> 21;
-        DecodePro pro{};
-        pro.chain = a.sync;
-        pro.link = l;
-        pro.epoch = epoch;
-        pro.hx = L.hx;
-        pro.hd = L.hd;
-        decode_body<MT, 0, 0, true, false, 0, false, 0, false, true>(
-            nullptr, nullptr, L.x, abits, L.w, Mall, N, K, L.d, nullptr, nullptr, nullptr, 1, IPW, RC, xwin,
-            IPW - (ir != 0), ir, 1, nullptr, pro, grid);
-    }
-    if (epoch == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch alone):
-        __syncthreads();         // the last workgroup to arrive clears every granule (all the others
-        __shared__ uint32_t last;  // are done reading), the start counter and the epoch
+    if (chain_late(epoch) == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch
+        __syncthreads();                     // alone): the last workgroup to arrive clears every granule (all
+        __shared__ uint32_t last;            // the others are done reading), the start counter and the epoch
         if (threadIdx.x == 0) {
             asm volatile("" ::"v"(started));  // this workgroup's start arrival has been performed
-            last = __hip_atomic_fetch_add(a.sync + 32 * FQ_CHAIN_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            last = __hip_atomic_fetch_add(sync + 32 * FQ_CHAIN_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                    gridDim.x - 1;
         }
         __syncthreads();
         if (last) {
-            for (uint32_t i = threadIdx.x; i < a.hand_bytes / 16; i += blockDim.x) a.hand[i] = make_uint4(0, 0, 0, 0);
+            for (uint32_t i = threadIdx.x; i < t.hand_bytes / 16; i += blockDim.x) t.hand[i] = make_uint4(0, 0, 0, 0);
             if (threadIdx.x < 8)
-                __hip_atomic_store(a.sync + 32 * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(sync + 32 * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (threadIdx.x == 0) {
-                __hip_atomic_store(a.sync + 32 * FQ_CHAIN_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(a.sync + 32 * FQ_CHAIN_EPOCH, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(sync + 32 * FQ_CHAIN_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -2262,7 +2320,7 @@ extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int
             l++;
             continue;
         }
-        ChainArgs a{};
+        ChainLink cl[FQ_CHAIN_MAX];
         size_t lds = 0, off = 0;
         for (int i = 0; i < r; i++) {
             const fq_chain_link &L = links[l + i];
@@ -2278,15 +2336,18 @@ extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int
                 hd = reinterpret_cast<uint64_t *>(hand + off);
                 off += chain_handoff_bytes(M, L.N);
             }
-            a.l[i] = ChainLink{L.x, (const uint32_t *)L.w_packed, L.d, hx[i], hd, pk.w0, pk.w1, pk.w2, pk.w3};
+            cl[i] = ChainLink{L.x, (const uint32_t *)L.w_packed, L.d, hx[i], hd, pk.w0, pk.w1, pk.w2, pk.w3};
             const size_t b = decode_lds_bytes(p, M, L.N, L.K);
             lds = b > lds ? b : lds;
         }
-        a.n = r;
-        a.sync = (uint32_t *)chain_ws;
-        a.hand = (uint4 *)hand;
-        a.hand_bytes = (uint32_t)hand_bytes;
-        hipLaunchKernelGGL((fq_gemm_decode_chain_kernel<4>), dim3(plans[0].grid), dim3(decode_waves(4) * 64), lds, s, a);
+        ChainTail t{};
+        for (int i = 1; i < r; i++) t.l[i - 1] = cl[i];
+        t.n = r;
+        t.hand = (uint4 *)hand;
+        t.hand_bytes = (uint32_t)hand_bytes;
+        hipLaunchKernelGGL((fq_gemm_decode_chain_kernel<4>), dim3(plans[0].grid), dim3(decode_waves(4) * 64), lds, s,
+                           (uint32_t *)chain_ws, cl[0].x, cl[0].w, cl[0].d, cl[0].w0, cl[0].w1, cl[0].w2, cl[0].w3,
+                           cl[0].hd, t);
         FQ_LAUNCH_CHECK();
         l += r;
     }

@@ -301,14 +301,19 @@ def linear_chain_w6ax(links):
     return [l[4] for l in links]
 
 
-def chain_error(device=None, stream=None):
-    """The decode chain's sticky error word in the stream's chain workspace (0: every in-kernel wait
-    ended in time; 1: one timed out and the results since are undefined)."""
+def chain_workspace_buffer(device=None, stream=None):
+    """The stream's chain workspace (None before its first chain call)."""
     dev = torch.device(device if device is not None else "cuda")
     if dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
     s = stream if stream is not None else torch.cuda.current_stream(dev)
-    buf = _CWS.get((dev, s.cuda_stream))
+    return _CWS.get((dev, ctypes.c_void_p(s.cuda_stream).value))  # (the key _stream() makes)
+
+
+def chain_error(device=None, stream=None):
+    """The decode chain's sticky error word in the stream's chain workspace (0: every in-kernel wait
+    ended in time; 1: one timed out and the results since are undefined)."""
+    buf = chain_workspace_buffer(device, stream)
     if buf is None:
         return 0
     off = int(_lib.load().fq_chain_error_offset())

@@ -148,7 +148,7 @@ def test_chain_sync_words_and_epoch_wrap(ops, dev):
     links = build(ops, dev, 1, LAYER_7B, seed=8)
     ops.linear_chain_w6ax(links)
     torch.cuda.synchronize()
-    buf = ops._CWS[(links[0][0].device, torch.cuda.current_stream(dev).cuda_stream)]
+    buf = ops.chain_workspace_buffer(dev)
     words = buf[:4096].view(torch.int32)  # sync words 128 B apart: 0..7 start counter, 8 epoch, 9 error
     e0 = int(words[8 * 32].item())
     assert e0 >= 1 and all(int(words[32 * s].item()) == 0 for s in range(8))
