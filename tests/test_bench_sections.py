@@ -55,3 +55,18 @@ def test_optional_section_failure_is_agreed_across_ranks():
         assert "error" in res[r]["first"], res[r]
         assert res[r]["second"] == {"sum": 3.0}
     assert "another rank" in res[0]["first"]["error"] and "out of memory" in res[1]["first"]["error"]
+
+
+def test_chain_runs_cut_at_the_attention_cores():
+    """bench.chain_runs: the step's linears in order, cut before every o_proj (the attention core sits
+    between qkv and o), so 32 LLaMA layers give qkv_0 | (o, gate_up, down, qkv) x 31 | o, gate_up, down."""
+    sys.path.insert(0, ROOT)
+    import bench
+    layer = lambda i: {n: dict(x=f"x{n}{i}", pk=f"w{n}{i}", Nl=1, abits=6, out=f"d{n}{i}")  # noqa: E731
+                       for n in ("qkv", "o", "gate_up", "down")}
+    runs = bench.chain_runs([layer(i) for i in range(32)])
+    assert len(runs) == 33
+    assert [r[1] for r in runs[0]] == ["wqkv0"]
+    assert [r[1] for r in runs[1]] == ["wo0", "wgate_up0", "wdown0", "wqkv1"]
+    assert [r[1] for r in runs[-1]] == ["wo31", "wgate_up31", "wdown31"]
+    assert sum(len(r) for r in runs) == 128

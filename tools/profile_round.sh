@@ -5,7 +5,7 @@ R=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof gpurun_out/profiles
 P=gpurun_out/profiles  # merged back by gpurun; copy into profiles/ afterwards
-B="python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers --no-extra-configs"
+B="python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers --no-extra-configs --no-reference-sweep"
 # 1. kernel trace + stats of the default bench (LLaMA-2-7B, M=1)
 echo "[profile_round] 1. kernel trace + stats of the default bench (LLaMA-2-7B, " ; date
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/kt -o run -- $B --steps 5 > gpurun_out/prof/kt.log 2>&1
@@ -14,7 +14,7 @@ python3 tools/trace_summary.py gpurun_out/prof/kt/run_kernel_trace.csv > $P/${R}
 grep '"metric"' gpurun_out/prof/kt.log | tail -1 > $P/${R}_bench_under_rocprof.json
 # 2. HBM traffic: FETCH_SIZE pass alone (no other counters), decode kernel only
 echo "[profile_round] 2. HBM traffic: FETCH_SIZE pass alone (no other counters)," ; date
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_decode -f csv -d gpurun_out/prof/pmc -o run -- $B --steps 2 --warmup 1 --roofline-reps 1 > gpurun_out/prof/pmc.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_decode -f csv -d gpurun_out/prof/pmc -o run -- $B --no-chain --steps 2 --warmup 1 --roofline-reps 1 > gpurun_out/prof/pmc.log 2>&1
 cp gpurun_out/prof/pmc/run_counter_collection.csv $P/${R}_pmc_fetch_size.csv
 python3 tools/pmc_summary.py $P/${R}_pmc_fetch_size.csv fq_gemm_decode llama2-7b-m1 $P/${R}_pmc_summary.json > /dev/null
 python3 - "$R" <<'PY'
@@ -23,7 +23,10 @@ p = f"gpurun_out/profiles/{sys.argv[1]}_pmc_summary.json"
 d = json.load(open(p))
 d.update(launch_pattern="qkv, o, gate_up (merged), down per layer", merged_gate_up=True,
          command="rocprofv3 --pmc FETCH_SIZE --kernel-trace --kernel-include-regex fq_gemm_decode -f csv -- "
-                 "python3 bench.py --cpu-budget 0 --no-fp16-compare --steps 2 --warmup 1 --roofline-reps 1")
+                 "python3 bench.py --cpu-budget 0 --no-fp16-compare --no-layers --no-extra-configs "
+                 "--no-reference-sweep --no-chain --steps 2 --warmup 1 --roofline-reps 1",
+         note="one launch per linear (--no-chain): the chain form's linears stream the same image bytes "
+              "per linear, plus 4 B per output element of hand-off granules")
 d["source"] = f"profiles/{sys.argv[1]}_pmc_fetch_size.csv"  # where it is committed
 json.dump(d, open(p, "w"), indent=1)
 PY
