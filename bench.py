@@ -641,6 +641,22 @@ def measure_single(ctx, name, merge, steps, warmup):
     stack = build_stack(cfg, ctx.rank, 1, ctx.dev, merge)
     replay = ctx.prepare(lambda: run_step(stack, M, 1), not ctx.a.no_graph)
     elapsed, ev_s = ctx.timed(replay, steps, warmup)
+    chain = None
+    if M <= 4 and not ctx.a.no_chain:  # the decode chains, as for the headline (taken when identical + faster)
+        last_out = linears(stack)[-1][1]["out"]
+        ref_bits = last_out.cpu().numpy().view(np.uint16).copy()
+        runs = chain_runs(stack)
+        replay_c = ctx.prepare(lambda: run_chains(runs), not ctx.a.no_graph)
+        el_c, ev_c = ctx.timed(replay_c, steps, warmup)
+        same = bool(np.array_equal(last_out.cpu().numpy().view(np.uint16), ref_bits))
+        err = ops.chain_error(ctx.dev, stream=ctx.stream)
+        chain = {"launches_per_step": len(runs), "ms_per_step": round(el_c / steps * 1e3, 4),
+                 "launches_ms_per_step": round(elapsed / steps * 1e3, 4), "bit_identical_to_launches": same,
+                 "wait_timed_out": bool(err)}
+        if same and not err and el_c < elapsed:
+            elapsed, ev_s = el_c, ev_c
+            chain["taken"] = True
+        del replay_c
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)
     out = {"what": f"BASELINE config: {desc}, the dependent linear stack of every layer, one HIP graph" +
                    (" (weights: the fq6 image + its int8 MFMA operands unpacked once at load, "
@@ -650,6 +666,8 @@ def measure_single(ctx, name, merge, steps, warmup):
            "value": round(flops_step * steps / elapsed / 1e12, 4), "unit": "TFLOPS-equiv",
            "tok_per_s": round(M * steps / elapsed, 2), "steps": steps, "warmup": warmup,
            "finite": bool(torch.isfinite(linears(stack)[-1][1]["out"].float()).all().item())}
+    if chain is not None:
+        out["decode_chain"] = chain
     if M > PREFILL_M:
         codes = {}
         for nm, p in linears(stack):
