@@ -1,17 +1,6 @@
 # scratch GPU job (development; rewritten per gpurun call)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/j9_tests.log 2>&1 || { tail -30 gpurun_out/j9_tests.log; exit 1; }
-tail -2 gpurun_out/j9_tests.log
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/j9_smoke.log 2>&1 || { tail -20 gpurun_out/j9_smoke.log; exit 1; }
-tail -2 gpurun_out/j9_smoke.log
-timeout -k 10 800 python -u bench.py > gpurun_out/j9_bench.json 2> gpurun_out/j9_bench.err || { tail -20 gpurun_out/j9_bench.err; exit 1; }
-python -c "
-import json; d=json.loads(open('gpurun_out/j9_bench.json').read().strip().splitlines()[-1])
-print('value', d['value'], 'ms', d['ms_per_step'], 'frac', d['roofline']['frac'], d['config']['decode_form'])
-print('chain', d.get('decode_chain'))
-for k in ('c3_llama2_7b_m16','c5_llama3_8b_prefill','c4_llama2_70b_1gpu'): print(k, {kk: d.get(k,{}).get(kk) for kk in ('ms_per_step','value','error','skipped','decode_chain')})
-vs=d.get('vs_reference_sweep',{}); print('sweep', vs.get('avg_speedup_vs_int8_by_M'), vs.get('avg_speedup_vs_fp16_by_M'), vs.get('error'))
-e=d.get('decoder_layers_e2e',{}); print('e2e', {m: (e.get(m) or {}).get('w6_ms_per_step') for m in ('M1','M16')}, e.get('error'))
-print('cpu', d.get('cpu_baseline'))
-"
+timeout -k 10 1100 bash tools/profile_round.sh r04 > gpurun_out/j10_prof.log 2>&1 || { tail -30 gpurun_out/j10_prof.log; exit 1; }
+tail -5 gpurun_out/j10_prof.log
+ls gpurun_out/profiles/
