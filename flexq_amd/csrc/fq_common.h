@@ -315,6 +315,9 @@ struct DecodePro {
     uint32_t epoch;         //   the launch's epoch (granule tags)
     const uint64_t *hx;     //   granules holding x (the previous linear's hand-off), or null: x is ready
     uint64_t *hd;           //   this linear's hand-off granules (null: the chain's last linear)
+    bool cwrite;            //   linear 0: wave 0 writes the chain's argument copy to LDS
+    uint32_t cdesc_lds;     //     at this LDS address,
+    uint32_t dvx, dvy;      //     this lane's two dwords of it
 };
 
 // ---- fq6 weight unpack ----------------------------------------------------------------------

@@ -105,6 +105,7 @@ __host__ __device__ inline int decode_wave_lds(int MT, int XS, int SS, int ng, i
     return b;
 }
 
+#define FQ_CSTAMP_LINKS 8
 #ifdef FQ_DEV_ABLATION
 // development timeline: per WG (wave 0) s_memrealtime stamps (100 MHz), tools/stamps.py
 __device__ unsigned long long g_fq_stamps[1024 * 8];
@@ -112,8 +113,16 @@ __device__ unsigned long long g_fq_stamps[1024 * 8];
     if ((ABL & 16) && threadIdx.x == 0 && blockIdx.x < 1024) {                       \
         g_fq_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
     }
+// decode chain timeline: per (WG, linear) wave-0 stamps 0 linear start, 1 ring issued, 2 input
+// quantized, 3 first block landed, 4 stream done, 5 linear end (tools/chain_stamps.py)
+__device__ unsigned long long g_fq_cstamps[1024 * FQ_CSTAMP_LINKS * 8];
+#define FQ_CSTAMP(k)                                                                                   \
+    if (CHN && threadIdx.x == 0 && blockIdx.x < 1024 && pro.link < FQ_CSTAMP_LINKS) {                  \
+        g_fq_cstamps[((long)blockIdx.x * FQ_CSTAMP_LINKS + pro.link) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    }
 #else
 #define FQ_STAMP(k)
+#define FQ_CSTAMP(k)
 #endif
 
 // ---- peer-store gather (column-parallel decode, fq_linear_w6ax_gather): each rank stores its output
@@ -377,6 +386,7 @@ __device__ __forceinline__ void decode_body(
     static_assert(!CHN || (FUSE && PRO == 0 && !GAT && !CH && !DBG), "the chain runs plain fused linears");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FQ_STAMP(0);
+    FQ_CSTAMP(0);
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -644,7 +654,10 @@ __device__ __forceinline__ void decode_body(
         const int j = M == 1 ? rg : rg / M, row = rg - j * M;
         return ((uint32_t)row * K + (uint32_t)(ga + j) * FQ_GROUP + qsub * 8) * (gr ? 4 : 2);
     };
-    uint4 xv0[4];  // a ready x's first 16 pairs: loaded ahead of the ring, so they arrive first
+    // a ready x's first 16 pairs are loaded ahead of the ring, so they return first.  (Granules are
+    // not: a first look at the hand-off ahead of the ring made every linear slower -- the ring issue
+    // behind those loads took up to 1.4 us longer)
+    uint4 xv0[4];
     if (CHN && !gr && n > 0) {
 #pragma unroll
         for (int u = 0; u < 4; u++)
@@ -669,6 +682,7 @@ __device__ __forceinline__ void decode_body(
         }
     }
     FQ_STAMP(1);
+    FQ_CSTAMP(1);
     if (GAT && FUSE && wfold) {
         gather_poll(pro.wgat, pro.werr, wid);
         if (n > 0) x_fetch(0);
@@ -721,6 +735,12 @@ __device__ __forceinline__ void decode_body(
                 x_store(c + 4 * u + (lane >> 4), codes, sh);
             }
         }
+        FQ_CSTAMP(2);
+    }
+    if (CHN && pro.cwrite && wid == 0) {  // (the chain's argument copy -> LDS; loaded long ago)
+        ds_write_b64(pro.cdesc_lds + lane * 8, make_uint2(pro.dvx, pro.dvy));
+    }
+    if (CHN) {
     } else if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
         if (GAT && wfold)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the window was issued after the ring)
@@ -835,7 +855,10 @@ __device__ __forceinline__ void decode_body(
                 const int later = (n - 1 - i) < (D - 1) ? (n - 1 - i) : (D - 1);
                 wait_ring<C::U, D>(later);  // this slot (and every older DMA, the staging included) landed
             }
-            if (i == 0) FQ_STAMP(2);
+            if (i == 0) {
+                FQ_STAMP(2);
+                FQ_CSTAMP(3);
+            }
             const uint32_t sp = lds_addr(ring + slot * C::SLOT);
             v2u p0 = ds_read_b64(sp + lane * 8);
             v2u p1 = ds_read_b64(sp + 512 + lane * 8);
@@ -982,11 +1005,13 @@ __device__ __forceinline__ void decode_body(
         }
     }
     FQ_STAMP(3);
+    FQ_CSTAMP(4);
     if constexpr (CHN) {  // (S = 1)
         if (eupd) chain_epoch_update(pro.chain, chain_late(pro.epoch), eseen, gridall);
         // the next linear's prologue reuses the LDS: every wave is past this one's
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        FQ_CSTAMP(5);
         return;
     }
     // GAT is a separate instantiation: the gather's branches and publish step cost the plain
@@ -1131,12 +1156,11 @@ constexpr int FQ_CHAIN_TAIL_OFF = 56;  // the tail's byte offset in the argument
 static_assert(sizeof(ChainLink) == 56 && FQ_CHAIN_TAIL_OFF + sizeof(ChainTail) <= 512,
               "the chain's argument copy is 64 lanes x 8 bytes");
 template <int MT>
-__device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLink &L, uint32_t epoch) {
+__device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLink &L, uint32_t epoch, DecodePro pro) {
     const int N = L.w0 & 0x1fffff, abits = (L.w0 >> 21) & 15, xwin = L.w0 >> 25;
     const int K = (L.w1 & 0x1fff) * FQ_GROUP;
     const int IPW = L.w2 & 0xffff, RC = L.w2 >> 16;
     const int Mall = L.w3 & 1023, ir = (L.w3 >> 10) & 2047, grid = L.w3 >> 21;
-    DecodePro pro{};
     pro.chain = sync;
     pro.link = l;
     pro.epoch = epoch;
@@ -1151,41 +1175,53 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_ke
     uint32_t *__restrict__ sync, const uint16_t *x0, const uint32_t *w0p, uint16_t *d0, uint32_t p0, uint32_t p1,
     uint32_t p2, uint32_t p3, uint64_t *hd0, const ChainTail t) {
     const int lane = threadIdx.x & 63;
+    // the argument block (512 B): loaded into two VGPRs per lane as the launch starts, written to LDS
+    // by wave 0 once linear 0's inputs have arrived (so nothing waits for it), read per linear from
+    // LDS (no wait on the memory counter, which would also wait for the previous linear's stores)
+    __shared__ __attribute__((aligned(16))) uint32_t cdesc[128];
     typedef const uint32_t __attribute__((address_space(4))) kdword;  // (the constant address space)
     const kdword *ka = (const kdword *)__builtin_amdgcn_kernarg_segment_ptr();
-    const uint32_t dvx = ka[2 * lane], dvy = ka[2 * lane + 1];
+    DecodePro p0r{};
+    p0r.dvx = ka[2 * lane];
+    p0r.dvy = ka[2 * lane + 1];
+    p0r.cwrite = true;
+    p0r.cdesc_lds = lds_addr(cdesc);
     // the launch's epoch (used through chain_late, a linear later)
     const uint32_t epoch = __hip_atomic_load(sync + 32 * FQ_CHAIN_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    chain_link<MT>(sync, 0, ChainLink{x0, w0p, d0, nullptr, hd0, p0, p1, p2, p3}, epoch);
+    chain_link<MT>(sync, 0, ChainLink{x0, w0p, d0, nullptr, hd0, p0, p1, p2, p3}, epoch, p0r);
     // this workgroup has read the epoch (its tags were stored): arrive on the start counter
-    uint32_t started = 0;  // (returned; waited for only in the wrapping launch)
     if (threadIdx.x == 0)
-        started = __hip_atomic_fetch_add(sync + 32 * (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    auto rd = [&](int k) -> uint32_t {  // dword k of the arguments (wave-uniform k)
-        return __builtin_amdgcn_readlane((k & 1) ? dvy : dvx, k >> 1);
+        __hip_atomic_fetch_add(sync + 32 * (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cb = lds_addr(cdesc);
+    auto rd2 = [&](int k) -> uint2 {  // dwords k, k + 1 of the arguments (k even), from LDS
+        uint2 v;
+        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cb + 4 * k) : "memory");
+        return make_uint2(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y));
     };
-    auto rd64 = [&](int k) -> uint64_t { return (uint64_t)rd(k) | ((uint64_t)rd(k + 1) << 32); };
     constexpr int T0 = FQ_CHAIN_TAIL_OFF / 4, LW = sizeof(ChainLink) / 4;
-    const int n = (int)rd(T0 + offsetof(ChainTail, n) / 4);
+    static_assert(T0 % 2 == 0 && LW % 2 == 0 && offsetof(ChainTail, n) % 8 == 4, "ds_read_b64 pairs");
+    const int n = (int)rd2(T0 + offsetof(ChainTail, n) / 4 - 1).y;
     for (int l = 1; l < n; l++) {
         const int b = T0 + (l - 1) * LW;
+        const uint2 a0 = rd2(b), a1 = rd2(b + 2), a2 = rd2(b + 4), a3 = rd2(b + 6), a4 = rd2(b + 8), a5 = rd2(b + 10),
+                    a6 = rd2(b + 12);
         ChainLink L;
-        L.x = reinterpret_cast<const uint16_t *>(rd64(b));
-        L.w = reinterpret_cast<const uint32_t *>(rd64(b + 2));
-        L.d = reinterpret_cast<uint16_t *>(rd64(b + 4));
-        L.hx = reinterpret_cast<const uint64_t *>(rd64(b + 6));
-        L.hd = reinterpret_cast<uint64_t *>(rd64(b + 8));
-        L.w0 = rd(b + 10);
-        L.w1 = rd(b + 11);
-        L.w2 = rd(b + 12);
-        L.w3 = rd(b + 13);
-        chain_link<MT>(sync, l, L, epoch);
+        L.x = reinterpret_cast<const uint16_t *>((uint64_t)a0.x | ((uint64_t)a0.y << 32));
+        L.w = reinterpret_cast<const uint32_t *>((uint64_t)a1.x | ((uint64_t)a1.y << 32));
+        L.d = reinterpret_cast<uint16_t *>((uint64_t)a2.x | ((uint64_t)a2.y << 32));
+        L.hx = reinterpret_cast<const uint64_t *>((uint64_t)a3.x | ((uint64_t)a3.y << 32));
+        L.hd = reinterpret_cast<uint64_t *>((uint64_t)a4.x | ((uint64_t)a4.y << 32));
+        L.w0 = a5.x;
+        L.w1 = a5.y;
+        L.w2 = a6.x;
+        L.w3 = a6.y;
+        chain_link<MT>(sync, l, L, epoch, DecodePro{});
     }
     if (chain_late(epoch) == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch
         __syncthreads();                     // alone): the last workgroup to arrive clears every granule (all
         __shared__ uint32_t last;            // the others are done reading), the start counter and the epoch
         if (threadIdx.x == 0) {
-            asm volatile("" ::"v"(started));  // this workgroup's start arrival has been performed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's start arrival has been performed
             last = __hip_atomic_fetch_add(sync + 32 * FQ_CHAIN_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                    gridDim.x - 1;
         }
@@ -2085,6 +2121,9 @@ extern "C" fq_status fq_workspace_init(void *workspace, size_t bytes, fq_stream_
 extern "C" int fq_dev_stamps(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fq_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
+extern "C" int fq_dev_chain_stamps(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fq_cstamps), (size_t)n * 8) == hipSuccess ? 0 : 1;
+}
 extern "C" int fq_dev_pb_stamps(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pb_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
@@ -2242,6 +2281,7 @@ static bool chain_plan(int M, const fq_chain_link &L, DecodePlan *p) {
     if (M > 4 || L.N % 16 || ((uintptr_t)L.x & 15) || ((uintptr_t)L.d & 3)) return false;
     *p = decode_plan(M, L.N, L.K, true);
     return p->fits && p->MT == 4 && p->S == 1 && p->NCH == 1 && p->grid == device_cus() &&
+           decode_lds_bytes(*p, M, L.N, L.K) + 1024 <= kLdsMax &&  // (+ the chain kernel's static LDS)
            (size_t)p->NT * (L.K / FQ_GROUP) * FQ_BLOCK < ((size_t)1 << 32);
 }
 static size_t chain_handoff_bytes(int M, int N) { return ((size_t)M * N * 4 + 255) & ~(size_t)255; }

@@ -1,0 +1,76 @@
+"""Decode-chain timeline (development tool; tools/libflexq_hip_abl.so).  Runs the bench's layer
+chain (o -> gate_up -> down -> qkv, LLaMA-2-7B, M = 1, each input the leading K values of the previous
+output) in a graph, then reads the per-(WG, linear) wave-0 stamps (s_memrealtime, 100 MHz): 0 linear
+start, 1 ring issued, 2 input quantized (after the in-kernel wait), 3 first block landed, 4 stream
+done, 5 linear end.  Prints, per linear, medians and spreads over the WGs (us, from the launch's
+first stamp) and the hand-off: from the last WG's stream end of linear l to each WG's input-ready
+time of linear l + 1."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from flexq_amd import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+from flexq_amd import ops  # noqa: E402
+
+SHAPES = [("o", 4096, 4096, 6), ("gate_up", 22016, 4096, 6), ("down", 4096, 11008, 6), ("qkv", 12288, 4096, 6)]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    L = _lib.load()
+    L.fq_dev_chain_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    NL, NS = 8, 8
+    x0 = torch.randn((1, 4096), dtype=torch.float16, device=dev, generator=g)
+    chains = []
+    for c in range(6):  # rotating weight sets (cold images, as in the step)
+        links, prev = [], x0
+        for (_, N, K, ab) in SHAPES:
+            wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+            ws = ((torch.rand((K // 128, N), device=dev, generator=g) + 0.5) / (18.5 * 1.04 * K ** 0.5)).half()
+            out = torch.empty((1, N), dtype=torch.float16, device=dev)
+            x = prev if prev is x0 else prev.view(-1)[:K].view(1, K)
+            links.append((x, ops.pack_w6(wq, ws), N, ab, out))
+            prev = out
+        chains.append(links)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        for ch in chains:
+            ops.linear_chain_w6ax(ch)
+    s.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        for i in range(12):
+            ops.linear_chain_w6ax(chains[i % len(chains)])
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    st = (ctypes.c_ulonglong * (1024 * NL * NS))()
+    assert L.fq_dev_chain_stamps(st, 1024 * NL * NS) == 0
+    a = np.frombuffer(st, dtype=np.uint64).reshape(1024, NL, NS)[:256, :len(SHAPES), :6].astype(np.int64)
+    t0 = a[:, 0, 0].min()
+    us = (a - t0) / 100.0  # 100 MHz -> us
+    print("per linear (us from the launch's first stamp): median over WGs [min .. max]")
+    names = ["start", "ring issued", "quantized", "first block", "stream done", "end"]
+    for li, (name, N, K, _) in enumerate(SHAPES):
+        row = "  ".join(f"{nm} {np.median(us[:, li, k]):7.2f} [{us[:, li, k].min():6.2f}..{us[:, li, k].max():6.2f}]"
+                        for k, nm in enumerate(names))
+        print(f"{name:8s} {N:6d}x{K:<6d} {row}")
+    for li in range(1, len(SHAPES)):
+        last = us[:, li - 1, 4].max()
+        ready = us[:, li, 2]
+        print(f"hand-off {SHAPES[li - 1][0]} -> {SHAPES[li][0]}: last producer stream done {last:7.2f}; "
+              f"input quantized median {np.median(ready) - last:+.2f} [{ready.min() - last:+.2f} .. {ready.max() - last:+.2f}] us; "
+              f"consumer first block {np.median(us[:, li, 3]) - last:+.2f}; ring issued (median) {np.median(us[:, li, 1]) - last:+.2f}")
+    print("launch span", f"{us[:, len(SHAPES) - 1, 5].max():.2f} us")
+
+
+if __name__ == "__main__":
+    main()
