@@ -166,3 +166,28 @@ def test_chain_sync_words_and_epoch_wrap(ops, dev):
         assert all(int(words[32 * s].item()) == 0 for s in range(8)) and int(words[10 * 32].item()) == 0
     tags = buf[4096:].view(torch.int32)[1::2]  # every granule's tag word
     assert bool(((tags >= 0) & (tags <= 2)).all().item())  # no tag older than the wrap survives
+
+
+def test_chain_error_word_fails_fast_and_recovers(ops, dev):
+    """With the chain workspace's error word set (a wait timed out earlier) every in-kernel wait
+    returns at once -- the chain finishes fast, results undefined, never a hang; cleared, the chain
+    computes the right bits again."""
+    import time
+    links = build(ops, dev, 1, LAYER_7B * 2, seed=12)
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    buf = ops.chain_workspace_buffer(dev)
+    words = buf[:4096].view(torch.int32)
+    words[9 * 32] = 1
+    t0 = time.time()
+    for _ in range(3):
+        ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    assert time.time() - t0 < 5.0
+    assert ops.chain_error(dev) == 1
+    words[9 * 32] = 0
+    for (*_, out) in links:
+        out.fill_(float("nan"))
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    check(ops, links, dev, "after clearing the error word")
