@@ -315,9 +315,13 @@ struct DecodePro {
     uint32_t epoch;         //   the launch's epoch (granule tags)
     const uint64_t *hx;     //   granules holding x (the previous linear's hand-off), or null: x is ready
     uint64_t *hd;           //   this linear's hand-off granules (null: the chain's last linear)
-    bool cwrite;            //   linear 0: wave 0 writes the chain's argument copy to LDS
-    uint32_t cdesc_lds;     //     at this LDS address,
-    uint32_t dvx, dvy;      //     this lane's two dwords of it
+    int cpro;               //   the linear's producer: 0 none, 1 residual add + RMSNorm, 2 SiLU * up
+    const uint64_t *hin;    //   granules holding `in` (the previous linear's hand-off), or null
+    uint64_t *hr;           //   RMSNorm: granules of res_out for a later linear (or null)
+    bool cwrite;            //   linear 0: wave 0 copies the chain's argument block to LDS at cdesc_lds:
+    uint32_t cdesc_lds;     //     plain chains: 512 B, loaded as the launch starts (dvx, dvy per lane);
+    uint64_t kargs;         //     producer chains: 1 KiB, loaded behind linear 0's ring from kargs
+    uint32_t dvx, dvy;
 };
 
 // ---- fq6 weight unpack ----------------------------------------------------------------------

@@ -15,6 +15,7 @@
 // weight layout stores exactly these B operands (16-column tiles, fq_quant.hip).
 #include "fq_lds.h"
 #include <cstdlib>
+#include <type_traits>
 
 // =============================================================================================
 // Decode / small-M kernel (M <= 32): HBM-bound weight streaming.
@@ -360,7 +361,7 @@ __device__ __forceinline__ void dequant4(float (&c)[4], v4i acc, __half2 p01, __
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
 template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0, bool GAT = false,
-          bool CHN = false>
+          bool CHN = false, bool CHP = false>
 __device__ __forceinline__ void decode_body(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
@@ -645,24 +646,36 @@ __device__ __forceinline__ void decode_body(
     // the chain: lane (pair c + 4u + lane / 16, chunk lane % 16) holds 8 fp16 values of x -- as 16 bytes
     // of x itself (an input ready before the launch: gr false), or as the four 8-byte granules of the
     // previous linear's hand-off (gr)
+    // A producer link reads a second source, `in` (RMSNorm: added to the residual x; SiLU: up), the same
+    // way; SiLU's gate and up rows have stride ldh.
     const bool gr = CHN && pro.hx != nullptr;
+    // (CHP: a chain launch whose run holds producer links -- a separate instantiation, so the plain
+    // chain keeps its code)
+    const int cpro = CHP ? pro.cpro : 0;
+    const bool hasin = CHP && cpro != 0 && pro.in != nullptr, gin = hasin && pro.hin != nullptr;
+    const uint32_t xld = CHP && cpro == 2 ? (uint32_t)pro.ldh : (uint32_t)K;  // row stride (elements)
+    const uint32_t xspan = (uint32_t)(M - 1) * xld + K;                           // elements of a source
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        gr ? (void *)pro.hx : (void *)xh, (short)0, (int)((uint32_t)M * K * (gr ? 4 : 2)), 0x00020000);
-    auto chn_off = [&](int c, int u) -> uint32_t {
+        gr ? (void *)pro.hx : (void *)xh, (short)0, (int)(xspan * (gr ? 4 : 2)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t inr = __builtin_amdgcn_make_buffer_rsrc(
+        gin ? (void *)pro.hin : (void *)pro.in, (short)0, (int)(xspan * (gin ? 4 : 2)), 0x00020000);
+    auto chn_el = [&](int c, int u) -> uint32_t {  // element offset of the lane's 8 values
         int rg = c + 4 * u + (lane >> 4);
         rg = rg < R ? rg : R - 1;
         const int j = M == 1 ? rg : rg / M, row = rg - j * M;
-        return ((uint32_t)row * K + (uint32_t)(ga + j) * FQ_GROUP + qsub * 8) * (gr ? 4 : 2);
+        return (uint32_t)row * xld + (uint32_t)(ga + j) * FQ_GROUP + qsub * 8;
     };
+    auto chn_off = [&](int c, int u) -> uint32_t { return chn_el(c, u) * (gr ? 4 : 2); };
     // a ready x's first 16 pairs are loaded ahead of the ring, so they return first.  (Granules are
     // not: a first look at the hand-off ahead of the ring made every linear slower -- the ring issue
     // behind those loads took up to 1.4 us longer)
-    uint4 xv0[4];
+    uint4 xv0[4], gg0 = make_uint4(0, 0, 0, 0);
     if (CHN && !gr && n > 0) {
 #pragma unroll
         for (int u = 0; u < 4; u++)
             if (4 * u < R) xv0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, chn_off(0, u), 0, 16));
     }
+    if (CHP && cpro == 1 && n > 0) gg0 = *reinterpret_cast<const uint4 *>(pro.gamma + chn_el(0, 0));  // (RMSNorm: gamma, likewise)
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
     auto advance = [&]() {
         if (++rj == ng) {
@@ -683,6 +696,15 @@ __device__ __forceinline__ void decode_body(
     }
     FQ_STAMP(1);
     FQ_CSTAMP(1);
+    // a producer chain's argument block, by wave 0 of linear 0 only, issued behind its ring (needed a
+    // linear later; a plain chain's smaller block was loaded as the launch started)
+    typedef const uint32_t __attribute__((address_space(4))) kdword;  // (the constant address space)
+    uint32_t dv[4] = {0u, 0u, 0u, 0u};
+    if (CHN && CHP && pro.cwrite && wid == 0) {
+        const kdword *ka = (const kdword *)(uintptr_t)pro.kargs + 4 * lane;
+#pragma unroll
+        for (int q = 0; q < 4; q++) dv[q] = ka[q];
+    }
     if (GAT && FUSE && wfold) {
         gather_poll(pro.wgat, pro.werr, wid);
         if (n > 0) x_fetch(0);
@@ -691,7 +713,7 @@ __device__ __forceinline__ void decode_body(
     const bool eupd = CHN && pro.link == 1 && blockIdx.x == 0 && wid == 0 && chain_late(pro.epoch) != 0xfffffffeu;
     const uint32_t eseen = eupd ? chain_epoch_load(pro.chain) : 0u;
 
-    if (CHN && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers; from the hand-off,
+    if (CHN && !CHP && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers; from the hand-off,
         // each lane's four granules re-loaded until every tag is this launch's tag
         const uint32_t want = gr ? chain_tag(chain_late(pro.epoch)) : 0u;
         uint32_t *err = pro.chain + 32 * FQ_CHAIN_ERR;
@@ -736,9 +758,94 @@ __device__ __forceinline__ void decode_body(
             }
         }
         FQ_CSTAMP(2);
+    } else if (CHP && n > 0) {  // ---- the chain with producer links (a separate instantiation): two sources
+        // each lane's four granules re-loaded until every tag is this launch's tag
+        const uint32_t want = (gr || gin) ? chain_tag(chain_late(pro.epoch)) : 0u;
+        uint32_t *err = pro.chain + 32 * FQ_CHAIN_ERR;
+        bool failed = (gr || gin) && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        for (int c = 0; c < R; c += 16) {  // wave-uniform
+            uint4 v[4], w[4];  // x (RMSNorm: the residual; SiLU: gate) and `in`
+#pragma unroll
+            for (int u = 0; u < 4; u++) w[u] = make_uint4(0, 0, 0, 0);
+            // one pass over both sources: ready values load once, granules until their tags match
+            for (int spin = 0; spin < (1 << 20); spin++) {
+                bool ok = true;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (c + 4 * u >= R) break;
+                    const uint32_t el = chn_el(c, u);
+                    if (!gr) {
+                        if (spin == 0) v[u] = c == 0 ? xv0[u] : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 2, 0, 16));
+                    } else {
+                        const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4, 0, 16));
+                        const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4 + 16, 0, 16));
+                        v[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
+                        ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                    }
+                    if (hasin && !gin) {
+                        if (spin == 0) w[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 2, 0, 16));
+                    } else if (gin) {
+                        const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4, 0, 16));
+                        const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4 + 16, 0, 16));
+                        w[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
+                        ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (spin == (1 << 20) - 1) {
+                    failed = true;
+                    if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (CHP && cpro == 1) {  // residual add + RMSNorm (M = 1, K = 4 x 128 x NW: lane = chunk 64 wid + lane,
+                                  // as the fused producer kernel, PRO 1 above -- the same bits)
+                uint4 r = v[0];
+                const uint4 gg = gg0;
+                if (hasin) {
+                    r = add_residual8(w[0], r);
+                    if (blockIdx.x == 0) {
+                        *reinterpret_cast<uint4 *>(pro.res_out + chn_el(0, 0)) = r;
+                        if (pro.hr) {  // the residual for a later linear of the chain: four granules
+                            const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+                            const uint64_t tg = (uint64_t)chain_tag(chain_late(pro.epoch)) << 32;
+#pragma unroll
+                            for (int q = 0; q < 4; q++)
+                                __hip_atomic_store(pro.hr + chn_el(0, 0) / 2 + q, tg | rw[q], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                }
+                float acc = wave_sum64(sumsq8(r, 0.0f));
+                if (lane == 0) ds_write_b32(lds_addr(wsum) + 4 * wid, __float_as_uint(acc));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                v4i s0 = ds_read_b128(lds_addr(wsum)), s1 = ds_read_b128(lds_addr(wsum) + 16);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s0), "+v"(s1)::"memory");
+                float ss = __int_as_float(s0[0]);
+#pragma unroll
+                for (int q = 1; q < NW; q++) ss = ss + __int_as_float(q < 4 ? s0[q] : s1[q - 4]);
+                uint2 codes;
+                const uint16_t sh = quant_group16(rms_apply8(r, gg, rms_scale(ss, K, pro.eps)), abits, codes);
+                x_store(lane >> 4, codes, sh);
+                break;  // (R = 4: one chunk)
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (c + 4 * u >= R) break;
+                uint2 codes;
+                const uint4 q = CHP && cpro == 2 ? silu_mul8(v[u], w[u]) : v[u];
+                const uint16_t sh = quant_group16(q, abits, codes);
+                x_store(c + 4 * u + (lane >> 4), codes, sh);
+            }
+        }
+        FQ_CSTAMP(2);
     }
-    if (CHN && pro.cwrite && wid == 0) {  // (the chain's argument copy -> LDS; loaded long ago)
-        ds_write_b64(pro.cdesc_lds + lane * 8, make_uint2(pro.dvx, pro.dvy));
+    if (CHN && pro.cwrite && wid == 0) {  // (the chain's argument copy -> LDS; landed with the inputs)
+        if (CHP)
+            ds_write_b128(pro.cdesc_lds + lane * 16, v4i{(int)dv[0], (int)dv[1], (int)dv[2], (int)dv[3]});
+        else
+            ds_write_b64(pro.cdesc_lds + lane * 8, make_uint2(pro.dvx, pro.dvy));
     }
     if (CHN) {
     } else if (FUSE && n > 0) {  // ---- codes -> x_st, scales -> xs_st
@@ -1131,32 +1238,57 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ln_kerne
 }
 
 // The decode chain's kernel: the links' packed fields (decode_pack) by value in the kernel
-// arguments (40 B per linear, read by scalar loads as each linear starts); every linear runs the
-// fused plan fq_linear_w6ax would run for it (S = 1, the same grid), so the bits are the same.
-struct ChainLink {
+// arguments (read from LDS as each linear starts); every linear runs the fused plan fq_linear_w6ax
+// would run for it (S = 1, the same grid), so the bits are the same.  Two argument layouts: a plain
+// chain's links (56 B) and a producer chain's (ChainLinkP, 104 B: the producer's operands too).
+struct ChainLinkP {
+    const uint16_t *x;       // plain: x; RMSNorm: the residual; SiLU: gate
+    const uint32_t *w;
+    uint16_t *d;
+    const uint64_t *hx;      // x's granules (the previous link's hand-off + offset, or an earlier RMSNorm
+                             // link's residual output), or null: x is ready
+    uint64_t *hd;            // this link's hand-off granules, or null
+    const uint16_t *in;      // RMSNorm: added to the residual (or null); SiLU: up
+    const uint64_t *hin;     // in's granules (the previous link's hand-off + offset), or null: ready
+    const uint16_t *gamma;   // RMSNorm
+    uint16_t *res_out;       // RMSNorm with in
+    uint64_t *hr;            // RMSNorm: granules of res_out for a later link, or null
+    uint32_t w0, w1, w2, w3;
+    float eps;
+    uint32_t ldh_pro;        // SiLU row stride (24 bits) | producer << 24
+};
+struct ChainLinkPlain {
     const uint16_t *x;
     const uint32_t *w;
     uint16_t *d;
-    const uint64_t *hx;  // x's granules (the previous link's hand-off + offset), or null: x is ready
-    uint64_t *hd;        // this link's hand-off granules, or null (the last link)
+    const uint64_t *hx;
+    uint64_t *hd;
     uint32_t w0, w1, w2, w3;
 };
-// The sync pointer and link 0 lead the arguments as scalars (the first 48 bytes preloaded into SGPRs
-// at wave start -- an aggregate argument is not --, link 0's hand-off pointer after them: it is read
-// at the epilogue; link 0 never reads granules); the other links follow in a struct, read from
-// a copy of the whole argument block that every wave loads into VGPRs as it starts (two dwords per
-// lane, v_readlane per field): no scalar round trip before the first DMA or between linears.
+// The sync pointer and link 0 (a plain linear) lead the arguments as scalars (the first 48 bytes
+// preloaded into SGPRs at wave start -- an aggregate argument is not --, link 0's hand-off pointer
+// after them: it is read at the epilogue); the other links follow in a struct.  A copy of the
+// argument block reaches VGPRs in linear 0 (plain: 512 B, two dwords per lane as every wave starts;
+// producer: 1 KiB, four dwords per lane of wave 0, behind its ring), wave 0 writes it to LDS once
+// linear 0's input has arrived (so nothing waits for it), and every later linear reads its link from
+// LDS (no wait on the memory counter, which would also wait for the previous linear's stores).
+template <class LINK, int PAD>
 struct ChainTail {
-    ChainLink l[FQ_CHAIN_MAX - 1];  // links 1 ..
-    uint4 *hand;                    // the hand-off region (cleared when the tag wraps)
+    LINK l[FQ_CHAIN_MAX - 1];  // links 1 ..
+    uint4 *hand;               // the hand-off region (cleared when the tag wraps)
     uint32_t hand_bytes;
-    int n;  // >= 2
+    int n;                     // >= 2
+    uint32_t pad[PAD];         // (producer: the argument block is >= 1 KiB, the copy reads 1 KiB)
 };
+typedef ChainTail<ChainLinkPlain, 1> ChainTailPlain;
+typedef ChainTail<ChainLinkP, 56> ChainTailP;
 constexpr int FQ_CHAIN_TAIL_OFF = 56;  // the tail's byte offset in the arguments
-static_assert(sizeof(ChainLink) == 56 && FQ_CHAIN_TAIL_OFF + sizeof(ChainTail) <= 512,
-              "the chain's argument copy is 64 lanes x 8 bytes");
-template <int MT>
-__device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLink &L, uint32_t epoch, DecodePro pro) {
+static_assert(sizeof(ChainLinkP) == 104 && FQ_CHAIN_TAIL_OFF + sizeof(ChainTailP) >= 1024 &&
+              FQ_CHAIN_TAIL_OFF + offsetof(ChainTailP, pad) <= 1024, "the producer copy is 64 lanes x 16 bytes");
+static_assert(sizeof(ChainLinkPlain) == 56 && FQ_CHAIN_TAIL_OFF + offsetof(ChainTailPlain, pad) <= 512,
+              "the plain copy is 64 lanes x 8 bytes");
+template <int MT, bool CHP>
+__device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLinkP &L, uint32_t epoch, DecodePro pro) {
     const int N = L.w0 & 0x1fffff, abits = (L.w0 >> 21) & 15, xwin = L.w0 >> 25;
     const int K = (L.w1 & 0x1fff) * FQ_GROUP;
     const int IPW = L.w2 & 0xffff, RC = L.w2 >> 16;
@@ -1166,29 +1298,49 @@ __device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLin
     pro.epoch = epoch;
     pro.hx = L.hx;
     pro.hd = L.hd;
-    decode_body<MT, 0, 0, true, false, 0, false, 0, false, true>(
+    if (CHP) {
+        pro.in = L.in;
+        pro.hin = L.hin;
+        pro.gamma = L.gamma;
+        pro.res_out = L.res_out;
+        pro.hr = L.hr;
+        pro.eps = L.eps;
+        pro.ldh = (int)(L.ldh_pro & 0xffffff);
+        pro.cpro = (int)(L.ldh_pro >> 24);
+    }
+    decode_body<MT, 0, 0, true, false, 0, false, 0, false, true, CHP>(
         nullptr, nullptr, L.x, abits, L.w, Mall, N, K, L.d, nullptr, nullptr, nullptr, 1, IPW, RC, xwin,
         IPW - (ir != 0), ir, 1, nullptr, pro, grid);
 }
-template <int MT>
+template <int MT, bool CHP>
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_kernel(
     uint32_t *__restrict__ sync, const uint16_t *x0, const uint32_t *w0p, uint16_t *d0, uint32_t p0, uint32_t p1,
-    uint32_t p2, uint32_t p3, uint64_t *hd0, const ChainTail t) {
-    const int lane = threadIdx.x & 63;
-    // the argument block (512 B): loaded into two VGPRs per lane as the launch starts, written to LDS
-    // by wave 0 once linear 0's inputs have arrived (so nothing waits for it), read per linear from
-    // LDS (no wait on the memory counter, which would also wait for the previous linear's stores)
-    __shared__ __attribute__((aligned(16))) uint32_t cdesc[128];
-    typedef const uint32_t __attribute__((address_space(4))) kdword;  // (the constant address space)
-    const kdword *ka = (const kdword *)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t p2, uint32_t p3, uint64_t *hd0, const std::conditional_t<CHP, ChainTailP, ChainTailPlain> t) {
+    typedef std::conditional_t<CHP, ChainLinkP, ChainLinkPlain> LINK;
+    __shared__ __attribute__((aligned(16))) uint32_t cdesc[CHP ? 256 : 128];
     DecodePro p0r{};
-    p0r.dvx = ka[2 * lane];
-    p0r.dvy = ka[2 * lane + 1];
+    p0r.kargs = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    if (!CHP) {
+        typedef const uint32_t __attribute__((address_space(4))) kdword;  // (the constant address space)
+        const kdword *ka = (const kdword *)__builtin_amdgcn_kernarg_segment_ptr();
+        const int lane = threadIdx.x & 63;
+        p0r.dvx = ka[2 * lane];
+        p0r.dvy = ka[2 * lane + 1];
+    }
     p0r.cwrite = true;
     p0r.cdesc_lds = lds_addr(cdesc);
     // the launch's epoch (used through chain_late, a linear later)
     const uint32_t epoch = __hip_atomic_load(sync + 32 * FQ_CHAIN_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    chain_link<MT>(sync, 0, ChainLink{x0, w0p, d0, nullptr, hd0, p0, p1, p2, p3}, epoch, p0r);
+    ChainLinkP L0{};
+    L0.x = x0;
+    L0.w = w0p;
+    L0.d = d0;
+    L0.hd = hd0;
+    L0.w0 = p0;
+    L0.w1 = p1;
+    L0.w2 = p2;
+    L0.w3 = p3;
+    chain_link<MT, CHP>(sync, 0, L0, epoch, p0r);
     // this workgroup has read the epoch (its tags were stored): arrive on the start counter
     if (threadIdx.x == 0)
         __hip_atomic_fetch_add(sync + 32 * (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1198,24 +1350,39 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_ke
         asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cb + 4 * k) : "memory");
         return make_uint2(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y));
     };
-    constexpr int T0 = FQ_CHAIN_TAIL_OFF / 4, LW = sizeof(ChainLink) / 4;
-    static_assert(T0 % 2 == 0 && LW % 2 == 0 && offsetof(ChainTail, n) % 8 == 4, "ds_read_b64 pairs");
-    const int n = (int)rd2(T0 + offsetof(ChainTail, n) / 4 - 1).y;
+    auto ptr = [&](int k) -> uint64_t {
+        const uint2 a = rd2(k);
+        return (uint64_t)a.x | ((uint64_t)a.y << 32);
+    };
+    typedef std::conditional_t<CHP, ChainTailP, ChainTailPlain> TAIL;
+    constexpr int T0 = FQ_CHAIN_TAIL_OFF / 4, LW = sizeof(LINK) / 4;
+    static_assert(T0 % 2 == 0 && LW % 2 == 0 && offsetof(TAIL, n) % 8 == 4, "ds_read_b64 pairs");
+    const int n = (int)rd2(T0 + offsetof(TAIL, n) / 4 - 1).y;
     for (int l = 1; l < n; l++) {
         const int b = T0 + (l - 1) * LW;
-        const uint2 a0 = rd2(b), a1 = rd2(b + 2), a2 = rd2(b + 4), a3 = rd2(b + 6), a4 = rd2(b + 8), a5 = rd2(b + 10),
-                    a6 = rd2(b + 12);
-        ChainLink L;
-        L.x = reinterpret_cast<const uint16_t *>((uint64_t)a0.x | ((uint64_t)a0.y << 32));
-        L.w = reinterpret_cast<const uint32_t *>((uint64_t)a1.x | ((uint64_t)a1.y << 32));
-        L.d = reinterpret_cast<uint16_t *>((uint64_t)a2.x | ((uint64_t)a2.y << 32));
-        L.hx = reinterpret_cast<const uint64_t *>((uint64_t)a3.x | ((uint64_t)a3.y << 32));
-        L.hd = reinterpret_cast<uint64_t *>((uint64_t)a4.x | ((uint64_t)a4.y << 32));
+        ChainLinkP L{};
+        L.x = reinterpret_cast<const uint16_t *>(ptr(b));
+        L.w = reinterpret_cast<const uint32_t *>(ptr(b + 2));
+        L.d = reinterpret_cast<uint16_t *>(ptr(b + 4));
+        L.hx = reinterpret_cast<const uint64_t *>(ptr(b + 6));
+        L.hd = reinterpret_cast<uint64_t *>(ptr(b + 8));
+        constexpr int WO = offsetof(LINK, w0) / 4;
+        if (CHP) {
+            L.in = reinterpret_cast<const uint16_t *>(ptr(b + 10));
+            L.hin = reinterpret_cast<const uint64_t *>(ptr(b + 12));
+            L.gamma = reinterpret_cast<const uint16_t *>(ptr(b + 14));
+            L.res_out = reinterpret_cast<uint16_t *>(ptr(b + 16));
+            L.hr = reinterpret_cast<uint64_t *>(ptr(b + 18));
+            const uint2 a7 = rd2(b + WO + 4);
+            L.eps = __uint_as_float(a7.x);
+            L.ldh_pro = a7.y;
+        }
+        const uint2 a5 = rd2(b + WO), a6 = rd2(b + WO + 2);
         L.w0 = a5.x;
         L.w1 = a5.y;
         L.w2 = a6.x;
         L.w3 = a6.y;
-        chain_link<MT>(sync, l, L, epoch, DecodePro{});
+        chain_link<MT, CHP>(sync, l, L, epoch, DecodePro{});
     }
     if (chain_late(epoch) == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch
         __syncthreads();                     // alone): the last workgroup to arrive clears every granule (all
@@ -2276,25 +2443,43 @@ fq_status fq_decode_linear_fused(const uint16_t *x, int M, int N, int K, int abi
 
 // ---- decode chain: the links that can run in one persistent launch are those whose fused plan
 // is one 4-row tile set over the whole chip with no k-split (every LLaMA / OPT decode shape at
-// M <= 4 with N >= 16 x CUs), outputs in 16-column multiples, 16-byte aligned activations.
-static bool chain_plan(int M, const fq_chain_link &L, DecodePlan *p) {
-    if (M > 4 || L.N % 16 || ((uintptr_t)L.x & 15) || ((uintptr_t)L.d & 3)) return false;
-    *p = decode_plan(M, L.N, L.K, true);
-    return p->fits && p->MT == 4 && p->S == 1 && p->NCH == 1 && p->grid == device_cus() &&
-           decode_lds_bytes(*p, M, L.N, L.K) + 1024 <= kLdsMax &&  // (+ the chain kernel's static LDS)
-           (size_t)p->NT * (L.K / FQ_GROUP) * FQ_BLOCK < ((size_t)1 << 32);
+// M <= 4 with N >= 16 x CUs), outputs in 16-column multiples, 16-byte aligned activations; a
+// producer link as its one-launch entry point requires (RMSNorm: M = 1, K = 4096; SiLU: any M <= 4).
+static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+    return a && b && (uintptr_t)a < (uintptr_t)b + nb && (uintptr_t)b < (uintptr_t)a + na;
 }
-static size_t chain_handoff_bytes(int M, int N) { return ((size_t)M * N * 4 + 255) & ~(size_t)255; }
 static bool in_range(const void *a, size_t na, const void *b, size_t nb) {  // [a, a+na) inside [b, b+nb)
     return (uintptr_t)a >= (uintptr_t)b && (uintptr_t)a + na <= (uintptr_t)b + nb;
 }
-static bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
-    return (uintptr_t)a < (uintptr_t)b + nb && (uintptr_t)b < (uintptr_t)a + na;
+static size_t chain_xspan(int M, const fq_chain_link &L) {  // bytes of x (and in): SiLU rows have stride ldh
+    const size_t ld = L.pro == 2 ? (size_t)L.ldh : (size_t)L.K;
+    return ((size_t)(M - 1) * ld + L.K) * 2;
 }
+static bool chain_plan(int M, const fq_chain_link &L, DecodePlan *p) {
+    if (M > 4 || L.N % 16 || ((uintptr_t)L.x & 15) || ((uintptr_t)L.d & 3) || L.pro < 0 || L.pro > 2) return false;
+    if (L.pro == 1) {  // as fq_rmsnorm_linear_w6ax's one-launch form
+        const size_t rb = (size_t)L.K * 2;
+        if (M != 1 || L.K != 4 * FQ_GROUP * decode_waves(4) || !L.gamma || (L.in && !L.res_out) ||
+            (((uintptr_t)L.gamma | (uintptr_t)L.in | (uintptr_t)L.res_out) & 15))
+            return false;
+        if (L.in && (ranges_overlap(L.res_out, rb, L.x, rb) || ranges_overlap(L.res_out, rb, L.in, rb) ||
+                     ranges_overlap(L.res_out, rb, L.gamma, rb)))
+            return false;
+    }
+    if (L.pro == 2 && (!L.in || L.ldh < L.K || L.ldh % 8 || ((uintptr_t)L.in & 15))) return false;
+    *p = decode_plan(M, L.N, L.K, true);
+    return p->fits && p->MT == 4 && p->S == 1 && p->NCH == 1 && p->grid == device_cus() &&
+           decode_lds_bytes(*p, M, L.N, L.K) + 2048 <= kLdsMax &&  // (+ the chain kernel's static LDS)
+           (size_t)p->NT * (L.K / FQ_GROUP) * FQ_BLOCK < ((size_t)1 << 32);
+}
+static size_t chain_handoff_bytes(int M, int N) { return ((size_t)M * N * 4 + 255) & ~(size_t)255; }
 
 extern "C" size_t fq_chain_workspace_bytes(const fq_chain_link *links, int n, int M) {
     size_t b = FQ_CHAIN_SYNC_BYTES;
-    for (int l = 0; links && l + 1 < n; l++) b += chain_handoff_bytes(M, links[l].N);
+    for (int l = 0; links && l < n; l++) {
+        if (l + 1 < n) b += chain_handoff_bytes(M, links[l].N);
+        if (links[l].pro == 1 && links[l].in) b += chain_handoff_bytes(M, links[l].K);  // its residual output
+    }
     return b;
 }
 
@@ -2302,6 +2487,19 @@ extern "C" fq_status fq_chain_workspace_init(void *chain_ws, size_t bytes, fq_st
     if (!bytes) return FQ_OK;
     if (!chain_ws) return FQ_ERR_NULL;
     return hipMemsetAsync(chain_ws, 0, bytes, (hipStream_t)stream) == hipSuccess ? FQ_OK : FQ_ERR_HIP;
+}
+
+// one link as its own entry point (the chain's fallback; the same bits)
+static fq_status chain_link_alone(const fq_chain_link &L, int M, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
+                                  size_t workspace_bytes, fq_stream_t stream) {
+    if (L.pro == 1)
+        return fq_rmsnorm_linear_w6ax(L.in, L.x, L.res_out, L.gamma, L.eps, M, L.N, L.K, L.abits, L.w_packed, L.d,
+                                      xq_buf, xs_buf, workspace, workspace_bytes, stream);
+    if (L.pro == 2)
+        return fq_silu_linear_w6ax(L.x, L.in, L.ldh, M, L.N, L.K, L.abits, L.w_packed, L.d, xq_buf, xs_buf, workspace,
+                                   workspace_bytes, stream);
+    return fq_linear_w6ax(L.x, M, L.N, L.K, L.abits, L.w_packed, L.d, xq_buf, xs_buf, workspace, workspace_bytes,
+                          stream);
 }
 
 extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int M, void *chain_ws,
@@ -2314,54 +2512,102 @@ extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int
         if (!L.x || !L.w_packed || !L.d) return FQ_ERR_NULL;
         if (L.N <= 0 || L.K <= 0 || L.K % FQ_GROUP) return FQ_ERR_SHAPE;
         if (L.abits != 6 && L.abits != 8) return FQ_ERR_BITS;
+        if (L.pro < 0 || L.pro > 2) return FQ_ERR_SHAPE;
     }
     const hipStream_t s = (hipStream_t)stream;
     const bool ws_ok = chain_ws && chain_ws_bytes >= FQ_CHAIN_SYNC_BYTES && ((uintptr_t)chain_ws & 255) == 0;
-    char *hand = (char *)chain_ws + FQ_CHAIN_SYNC_BYTES;  // the hand-off granules of a run, link after link
+    char *hand = (char *)chain_ws + FQ_CHAIN_SYNC_BYTES;  // the hand-off granules of a run
     const size_t hand_bytes = ws_ok ? (chain_ws_bytes - FQ_CHAIN_SYNC_BYTES) / 16 * 16 : 0;
     if (hand_bytes >= ((size_t)1 << 32)) return FQ_ERR_WORKSPACE;
     int l = 0;
     while (l < n) {
-        // the longest run from l (at most FQ_CHAIN_MAX links) in which every link is chainable, the
-        // outputs are disjoint, and each link's x either lies inside the previous link's output (read
-        // from its hand-off granules) or overlaps no output of the run (ready before the launch)
+        // The longest run from l (at most FQ_CHAIN_MAX links, the first a plain linear) in which every
+        // link is chainable, no output (d, res_out) overlaps another output or any input (x, in, gamma)
+        // of the run, except that a link's x / in may lie inside the previous link's d (read from its
+        // hand-off granules) and an RMSNorm link's residual x may be an earlier RMSNorm link's res_out
+        // (read from that link's residual granules); every other input is ready before the launch.
         DecodePlan plans[FQ_CHAIN_MAX];
-        const uint64_t *hx[FQ_CHAIN_MAX] = {};
-        int r = 0;
+        int xsrc[FQ_CHAIN_MAX], insrc[FQ_CHAIN_MAX];  // -1 ready; j >= 0: link j's d (x, in) or res_out (x, RMSNorm)
+        bool needd[FQ_CHAIN_MAX] = {}, needr[FQ_CHAIN_MAX] = {};
         size_t used = 0;
-        while (ws_ok && l + r < n && r < FQ_CHAIN_MAX && chain_plan(M, links[l + r], &plans[r])) {
+        int r = 0;
+        while (ws_ok && l + r < n && r < FQ_CHAIN_MAX && (r > 0 || links[l].pro == 0) &&
+               chain_plan(M, links[l + r], &plans[r])) {
             const fq_chain_link &L = links[l + r];
-            const size_t xb = (size_t)M * L.K * 2, db = (size_t)M * L.N * 2;
-            bool ok = true, inside = false;
+            const size_t xb = chain_xspan(M, L), db = (size_t)M * L.N * 2, gb = (size_t)L.K * 2;
+            const size_t rb = (L.pro == 1 && L.in) ? (size_t)M * L.K * 2 : 0;  // res_out
+            int xs = -1, is = -1;
+            size_t extra = 0;
             if (r > 0) {
                 const fq_chain_link &P = links[l + r - 1];
-                inside = in_range(L.x, xb, P.d, (size_t)M * P.N * 2) && (((uintptr_t)L.x - (uintptr_t)P.d) & 3) == 0;
-                if (inside && used + chain_handoff_bytes(M, P.N) > hand_bytes) ok = false;
+                const size_t pb = (size_t)M * P.N * 2;
+                if (in_range(L.x, xb, P.d, pb) && (((uintptr_t)L.x - (uintptr_t)P.d) & 3) == 0) xs = r - 1;
+                if (L.pro != 0 && L.in && in_range(L.in, xb, P.d, pb) && (((uintptr_t)L.in - (uintptr_t)P.d) & 3) == 0)
+                    is = r - 1;
+                if ((xs >= 0 || is >= 0) && !needd[r - 1]) extra += chain_handoff_bytes(M, P.N);
             }
-            for (int i = 0; ok && i <= r; i++) {
-                const fq_chain_link &Q = links[l + i];
-                const size_t qb = (size_t)M * Q.N * 2;
-                if (i < r && ranges_overlap(L.d, db, Q.d, qb)) ok = false;      // disjoint outputs
-                if (i < r && ranges_overlap(Q.x, (size_t)M * Q.K * 2, L.d, db)) ok = false;  // no earlier x
-                if (!(inside && i == r - 1) && ranges_overlap(L.x, xb, Q.d, qb)) ok = false;  // x: hand-off or ready
+            if (xs < 0 && L.pro == 1)
+                for (int j = 0; j < r; j++)
+                    if (links[l + j].pro == 1 && links[l + j].in && links[l + j].res_out == L.x) {
+                        xs = FQ_CHAIN_MAX + j;  // (an earlier link's residual output)
+                        if (!needr[j]) extra += chain_handoff_bytes(M, links[l + j].K);
+                    }
+            bool ok = used + extra <= hand_bytes;
+            for (int j = 0; ok && j <= r; j++) {
+                const fq_chain_link &Q = links[l + j];
+                const size_t qd = (size_t)M * Q.N * 2, qr = (Q.pro == 1 && Q.in) ? (size_t)M * Q.K * 2 : 0;
+                const size_t qx = chain_xspan(M, Q);
+                // this link's outputs against every output and input of the run so far (itself included:
+                // its own res_out was checked by chain_plan)
+                if (j < r && (ranges_overlap(L.d, db, Q.d, qd) || ranges_overlap(L.d, db, Q.res_out, qr) ||
+                              ranges_overlap(L.res_out, rb, Q.d, qd) || ranges_overlap(L.res_out, rb, Q.res_out, qr)))
+                    ok = false;
+                if (ranges_overlap(L.d, db, Q.x, qx) || ranges_overlap(L.d, db, Q.in, Q.pro ? qx : 0) ||
+                    ranges_overlap(L.d, db, Q.gamma, Q.pro == 1 ? (size_t)Q.K * 2 : 0))
+                    ok = false;
+                if (j < r && (ranges_overlap(L.res_out, rb, Q.x, qx) || ranges_overlap(L.res_out, rb, Q.in, Q.pro ? qx : 0) ||
+                              ranges_overlap(L.res_out, rb, Q.gamma, Q.pro == 1 ? (size_t)Q.K * 2 : 0)))
+                    ok = false;
+                // this link's ready inputs against the run's outputs (its own included)
+                const bool xfrom = (xs == r - 1 && j == r - 1) || (xs == FQ_CHAIN_MAX + j);
+                if (!xfrom && (ranges_overlap(L.x, xb, Q.d, qd) || ranges_overlap(L.x, xb, Q.res_out, qr))) ok = false;
+                if (L.pro != 0 && !(is == r - 1 && j == r - 1) &&
+                    (ranges_overlap(L.in, xb, Q.d, qd) || ranges_overlap(L.in, xb, Q.res_out, qr)))
+                    ok = false;
+                if (L.pro == 1 && (ranges_overlap(L.gamma, gb, Q.d, qd) || ranges_overlap(L.gamma, gb, Q.res_out, qr)))
+                    ok = false;
             }
             if (!ok) break;
-            if (inside) {
-                hx[r] = reinterpret_cast<const uint64_t *>(hand + used) + ((uintptr_t)L.x - (uintptr_t)links[l + r - 1].d) / 4;
-                used += chain_handoff_bytes(M, links[l + r - 1].N);
-            }
+            xsrc[r] = xs;
+            insrc[r] = is;
+            if (xs >= 0 && xs < FQ_CHAIN_MAX) needd[xs] = true;
+            if (is >= 0) needd[is] = true;
+            if (xs >= FQ_CHAIN_MAX) needr[xs - FQ_CHAIN_MAX] = true;
+            used += extra;
             r++;
         }
-        if (r < 2) {  // a run of one is a plain linear
-            const fq_chain_link &L = links[l];
-            const fq_status st = fq_linear_w6ax(L.x, M, L.N, L.K, L.abits, L.w_packed, L.d, xq_buf, xs_buf, workspace,
-                                                workspace_bytes, stream);
+        if (r < 2) {  // a run of one: the link's own entry point
+            const fq_status st = chain_link_alone(links[l], M, xq_buf, xs_buf, workspace, workspace_bytes, stream);
             if (st != FQ_OK) return st;
             l++;
             continue;
         }
-        ChainLink cl[FQ_CHAIN_MAX];
-        size_t lds = 0, off = 0;
+        // hand-off regions: link i's output granules (when the next link reads its d), its residual
+        // granules (when a later RMSNorm link reads its res_out)
+        uint64_t *hd[FQ_CHAIN_MAX] = {}, *hr[FQ_CHAIN_MAX] = {};
+        size_t off = 0;
+        for (int i = 0; i < r; i++) {
+            if (needd[i]) {
+                hd[i] = reinterpret_cast<uint64_t *>(hand + off);
+                off += chain_handoff_bytes(M, links[l + i].N);
+            }
+            if (needr[i]) {
+                hr[i] = reinterpret_cast<uint64_t *>(hand + off);
+                off += chain_handoff_bytes(M, links[l + i].K);
+            }
+        }
+        ChainLinkP cl[FQ_CHAIN_MAX];
+        size_t lds = 0;
         for (int i = 0; i < r; i++) {
             const fq_chain_link &L = links[l + i];
             const DecodePlan &p = plans[i];
@@ -2370,24 +2616,44 @@ extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int
             if (items / p.grid != p.IPW - (items % p.grid != 0) ||
                 !decode_pack(L.N, L.K, L.abits, p.xwin, 1, 1, p.IPW, p.RC, M, items % p.grid, p.grid, &pk))
                 return FQ_ERR_SHAPE;
-            // a link's hand-off exists when the next link reads it; the granule offsets assigned above
-            uint64_t *hd = nullptr;
-            if (i + 1 < r && hx[i + 1]) {
-                hd = reinterpret_cast<uint64_t *>(hand + off);
-                off += chain_handoff_bytes(M, L.N);
+            const uint64_t *hx = nullptr, *hin = nullptr;
+            if (xsrc[i] >= FQ_CHAIN_MAX) {
+                hx = hr[xsrc[i] - FQ_CHAIN_MAX];
+            } else if (xsrc[i] >= 0) {
+                hx = hd[i - 1] + ((uintptr_t)L.x - (uintptr_t)links[l + i - 1].d) / 4;
             }
-            cl[i] = ChainLink{L.x, (const uint32_t *)L.w_packed, L.d, hx[i], hd, pk.w0, pk.w1, pk.w2, pk.w3};
+            if (insrc[i] >= 0) hin = hd[i - 1] + ((uintptr_t)L.in - (uintptr_t)links[l + i - 1].d) / 4;
+            cl[i] = ChainLinkP{L.x, (const uint32_t *)L.w_packed, L.d, hx, hd[i], L.pro ? L.in : nullptr, hin,
+                              L.pro == 1 ? L.gamma : nullptr, (L.pro == 1 && L.in) ? L.res_out : nullptr, hr[i],
+                              pk.w0, pk.w1, pk.w2, pk.w3, L.eps,
+                              (uint32_t)(L.pro == 2 ? L.ldh : 0) | ((uint32_t)L.pro << 24)};
             const size_t b = decode_lds_bytes(p, M, L.N, L.K);
             lds = b > lds ? b : lds;
         }
-        ChainTail t{};
-        for (int i = 1; i < r; i++) t.l[i - 1] = cl[i];
-        t.n = r;
-        t.hand = (uint4 *)hand;
-        t.hand_bytes = (uint32_t)hand_bytes;
-        hipLaunchKernelGGL((fq_gemm_decode_chain_kernel<4>), dim3(plans[0].grid), dim3(decode_waves(4) * 64), lds, s,
-                           (uint32_t *)chain_ws, cl[0].x, cl[0].w, cl[0].d, cl[0].w0, cl[0].w1, cl[0].w2, cl[0].w3,
-                           cl[0].hd, t);
+        bool prod = false;
+        for (int i = 0; i < r; i++) prod = prod || links[l + i].pro != 0;
+        if (prod) {
+            ChainTailP t{};
+            for (int i = 1; i < r; i++) t.l[i - 1] = cl[i];
+            t.n = r;
+            t.hand = (uint4 *)hand;
+            t.hand_bytes = (uint32_t)hand_bytes;
+            hipLaunchKernelGGL((fq_gemm_decode_chain_kernel<4, true>), dim3(plans[0].grid), dim3(decode_waves(4) * 64),
+                               lds, s, (uint32_t *)chain_ws, cl[0].x, cl[0].w, cl[0].d, cl[0].w0, cl[0].w1, cl[0].w2,
+                               cl[0].w3, cl[0].hd, t);
+        } else {
+            ChainTailPlain t{};
+            for (int i = 1; i < r; i++) {
+                const ChainLinkP &c = cl[i];
+                t.l[i - 1] = ChainLinkPlain{c.x, c.w, c.d, c.hx, c.hd, c.w0, c.w1, c.w2, c.w3};
+            }
+            t.n = r;
+            t.hand = (uint4 *)hand;
+            t.hand_bytes = (uint32_t)hand_bytes;
+            hipLaunchKernelGGL((fq_gemm_decode_chain_kernel<4, false>), dim3(plans[0].grid), dim3(decode_waves(4) * 64),
+                               lds, s, (uint32_t *)chain_ws, cl[0].x, cl[0].w, cl[0].d, cl[0].w0, cl[0].w1, cl[0].w2,
+                               cl[0].w3, cl[0].hd, t);
+        }
         FQ_LAUNCH_CHECK();
         l += r;
     }

@@ -178,6 +178,53 @@ class FlexQDecoderLayer:
         return h
 
 
+def run_layers_chained(layers, h):
+    """run_layers on one rank as decode chains (ops.linear_chain_w6ax), the same bits: the first
+    layer's RMSNorm + qkv alone, then per layer one chain o_i -> RMSNorm + gate_up_i -> SiLU * up +
+    down_i -> RMSNorm + qkv_i+1 (the last layer's without the qkv): the linears between two attention
+    cores in one persistent launch where the chain allows it (M = 1 for the norms), their entry points
+    otherwise.  The attention core (attn_fn) must return a view of its input or a tensor computed
+    before the chain (as the bench's stand-in ctx = v does): a chain cannot run a kernel between its
+    links.  The residual rotates through three buffers (h and two scratch), since a chain reads one and
+    writes two.  Returns h."""
+    if dist.is_initialized() and any(L.o.row_parallel and dist.get_world_size(L.o.group) > 1 for L in layers):
+        raise ValueError("run_layers_chained is single-rank (tensor parallelism needs the all-reduces between links)")
+    if not layers:
+        return h
+    M, H = h.shape
+    dev = h.device
+    res = [h, torch.empty_like(h), torch.empty_like(h)]
+    r = 0  # res[r] holds the current residual value
+    L0 = layers[0]
+    qkv = torch.empty((M, L0.qkv.N), dtype=torch.float16, device=dev)
+    ops.rmsnorm_linear_w6ax(res[r], L0.gamma_attn, L0.qkv.image, L0.qkv.N, L0.qkv.abits, eps=L0.eps, out=qkv)
+    pending = None
+    for i, L in enumerate(layers):
+        F = L.ffn.F
+        ctx = L.attn_fn(qkv)
+        if not ctx.is_contiguous():
+            ctx = ctx.contiguous()
+        a = torch.empty((M, L.o.N), dtype=torch.float16, device=dev)
+        gu = torch.empty((M, L.ffn.gate_up.N), dtype=torch.float16, device=dev)
+        y = torch.empty((M, L.ffn.down.N), dtype=torch.float16, device=dev)
+        r1, r2 = (r + 1) % 3, (r + 2) % 3
+        links = [(ctx, L.o.image, L.o.N, L.o.abits, a),
+                 ops.chain_rmsnorm(res[r], L.ffn.gamma, L.ffn.gate_up.image, L.ffn.gate_up.N, L.ffn.gate_up.abits, gu,
+                                   input=a, residual_out=res[r1], eps=L.ffn.eps),
+                 ops.chain_silu(gu[:, :F], gu[:, F:], L.ffn.down.image, L.ffn.down.N, L.ffn.down.abits, y)]
+        if i + 1 < len(layers):
+            Ln = layers[i + 1]
+            qkv = torch.empty((M, Ln.qkv.N), dtype=torch.float16, device=dev)
+            links.append(ops.chain_rmsnorm(res[r1], Ln.gamma_attn, Ln.qkv.image, Ln.qkv.N, Ln.qkv.abits, qkv,
+                                           input=y, residual_out=res[r2], eps=Ln.eps))
+            r = r2
+        else:
+            r, pending = r1, y
+        ops.linear_chain_w6ax(links)
+    torch.add(res[r], pending, out=h)  # (res[r] may be h itself: an elementwise in-place add)
+    return h
+
+
 def run_layers(layers, h, reduce=True):
     """Run decoder layers in order on h (in place), each layer's final residual add fused into the
     next layer's pre-attention norm, the norms and SiLU * up fused into their GEMMs

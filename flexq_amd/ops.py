@@ -257,48 +257,101 @@ def linear_w6ax(x, wpk, N, abits=6, out=None, w_u8=None):
 
 class _ChainLink(ctypes.Structure):  # fq_chain_link (include/flexq_hip.h)
     _fields_ = [("x", ctypes.c_void_p), ("w_packed", ctypes.c_void_p), ("d", ctypes.c_void_p),
-                ("N", ctypes.c_int), ("K", ctypes.c_int), ("abits", ctypes.c_int)]
+                ("N", ctypes.c_int), ("K", ctypes.c_int), ("abits", ctypes.c_int), ("pro", ctypes.c_int),
+                ("in_", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("res_out", ctypes.c_void_p),
+                ("eps", ctypes.c_float), ("ldh", ctypes.c_int)]
+
+
+def chain_rmsnorm(residual, gamma, wpk, N, abits, out, input=None, residual_out=None, eps=1e-6):
+    """A chain link computed as rmsnorm_linear_w6ax(residual, gamma, wpk, N, abits, eps, input,
+    residual_out, out) (residual_out required with input)."""
+    return dict(kind="rmsnorm", x=residual, gamma=gamma, w=wpk, N=N, abits=abits, out=out, input=input,
+                residual_out=residual_out, eps=eps)
+
+
+def chain_silu(gate, up, wpk, N, abits, out):
+    """A chain link computed as silu_linear_w6ax(gate, up, wpk, N, abits, out)."""
+    return dict(kind="silu", x=gate, up=up, w=wpk, N=N, abits=abits, out=out)
 
 
 def linear_chain_w6ax(links):
-    """Consecutive decode linears (fq_linear_chain_w6ax): links = [(x, wpk, N, abits, out), ...], each
-    computed exactly as linear_w6ax(x, wpk, N, abits, out=out), in order; x may be a view of an
-    earlier link's out (the chain's dependency).  Runs of chainable links (M <= 4) are
-    one persistent launch each.  Returns the list of outputs."""
+    """Consecutive decode linears (fq_linear_chain_w6ax), each computed exactly as its own call would be,
+    in order: a tuple (x, wpk, N, abits, out) is linear_w6ax(x, wpk, N, abits, out=out); chain_rmsnorm(...)
+    and chain_silu(...) are rmsnorm_linear_w6ax / silu_linear_w6ax.  An input may be a view of the previous
+    link's out, and an RMSNorm link's residual an earlier RMSNorm link's residual_out (the chain's
+    hand-offs).  Runs that can chain (M <= 4; RMSNorm at M = 1, K = 4096) are one
+    persistent launch each.  Returns the list of outputs."""
     _need(len(links) > 0, "empty chain")
-    M = None
+    M, dev, scratch, Kmax = None, None, 0, 0
     arr = (_ChainLink * len(links))()
-    scratch = 0
-    for i, (x, wpk, N, abits, out) in enumerate(links):
-        _dev(x, torch.float16, "x", 2)
+    outs = []
+    for i, lk in enumerate(links):
+        if isinstance(lk, dict):
+            kind = lk["kind"]
+            x, wpk, N, abits, out = lk["x"], lk["w"], lk["N"], lk["abits"], lk["out"]
+        else:
+            kind = "linear"
+            x, wpk, N, abits, out = lk
+        _need(isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float16 and x.dim() == 2,
+              "x must be a 2-D fp16 HIP tensor")
         m, K = x.shape
-        _need(x.stride(1) == 1 and x.stride(0) == K, "x must be a contiguous [M, K] row block")
+        _need(x.stride(1) == 1, "x rows must be contiguous")
         M = m if M is None else M
+        dev = x.device if dev is None else dev
         _need(m == M, "every link has the same M")
         _k_ok(K)
         _img_ok(wpk, N, K)
         _need(abits in (6, 8), "abits must be 6 or 8")
         _dev(out, torch.float16, "out", 2)
         _need(tuple(out.shape) == (M, N), f"out must be [M, N] = {(M, N)}")
-        _need(wpk.device == x.device == out.device == links[0][0].device, "one device")
-        _need(not _overlap(out, x), "a link's output must not overlap its input")
-        arr[i] = _ChainLink(_ptr(x), _ptr(wpk), _ptr(out), N, K, abits)
-        scratch = max(scratch, act_scratch_bytes(M, N, K) and M * K)
-    dev = links[0][0].device
+        _need(wpk.device == x.device == out.device == dev, "one device")
+        c = _ChainLink(x=_ptr(x), w_packed=_ptr(wpk), d=_ptr(out), N=N, K=K, abits=abits, pro=0, eps=0.0, ldh=0)
+        if kind == "linear":
+            _need(M == 1 or x.stride(0) == K, "x must be a contiguous [M, K] row block")
+            _need(not _overlap(out, x), "a link's output must not overlap its input")
+            sb = act_scratch_bytes(M, N, K)
+        elif kind == "rmsnorm":
+            gamma, inp, ro = lk["gamma"], lk["input"], lk["residual_out"]
+            _need(M == 1 or x.stride(0) == K, "the residual must be a contiguous [M, K] row block")
+            _dev(gamma, torch.float16, "gamma", 1)
+            _need(gamma.numel() == K and gamma.device == dev, "gamma must be [K] on the residual's device")
+            if inp is not None:
+                _dev(inp, torch.float16, "input", 2)
+                _need(tuple(inp.shape) == (M, K) and (M == 1 or inp.stride(0) == K), "input must match residual")
+                _dev(ro, torch.float16, "residual_out", 2)
+                _need(tuple(ro.shape) == (M, K), "residual_out must match residual")
+                for name, t in (("residual", x), ("input", inp), ("gamma", gamma)):
+                    _need(not _overlap(ro, t), f"residual_out must not overlap {name}")
+            c.pro, c.gamma, c.eps = 1, _ptr(gamma), float(lk["eps"])
+            c.in_, c.res_out = _ptr(inp), _ptr(ro if inp is not None else None)
+            sb = int(_lib.load().fq_rmsnorm_linear_scratch_bytes(M, N, K))
+        elif kind == "silu":
+            up = lk["up"]
+            _need(isinstance(up, torch.Tensor) and up.is_cuda and up.dtype == torch.float16 and up.device == dev,
+                  "up must be an fp16 HIP tensor on x's device")
+            _need(up.shape == x.shape and up.stride(0) == x.stride(0) and up.stride(1) == 1,
+                  "gate and up must have one shape and row stride")
+            c.pro, c.in_, c.ldh = 2, _ptr(up), (x.stride(0) if M > 1 else K)
+            sb = int(_lib.load().fq_silu_linear_scratch_bytes(M, N, K))
+        else:
+            raise ValueError(f"unknown chain link kind {kind!r}")
+        arr[i] = c
+        scratch, Kmax = max(scratch, sb), max(Kmax, K)
+        outs.append(out)
     xq = xs = None
     if scratch:
-        Kmax = max(x.shape[1] for (x, *_r) in links)
         xq = torch.empty((M, Kmax), dtype=torch.int8, device=dev)
         xs = torch.empty((Kmax // GROUP, M), dtype=torch.float16, device=dev)
-    s = _stream(links[0][0])
+    x0 = links[0]["x"] if isinstance(links[0], dict) else links[0][0]
+    s = _stream(x0)
     cb = int(_lib.load().fq_chain_workspace_bytes(ctypes.cast(arr, ctypes.c_void_p), len(links), M))
     cbuf = chain_workspace(dev, cb, s.value)
-    nb = max(gemm_workspace_bytes(M, N, x.shape[1]) for (x, _w, N, _a, _o) in links)
+    nb = max(gemm_workspace_bytes(M, c.N, c.K) for c in arr)
     wbuf = workspace(dev, nb, s.value)
     _lib.call("fq_linear_chain_w6ax", ctypes.cast(arr, ctypes.c_void_p), len(links), M, _ptr(cbuf),
               ctypes.c_size_t(cbuf.numel()), _ptr(xq), _ptr(xs), _ptr(wbuf),
               ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
-    return [l[4] for l in links]
+    return outs
 
 
 def chain_workspace_buffer(device=None, stream=None):

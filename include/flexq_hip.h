@@ -126,15 +126,17 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
                          size_t workspace_bytes, fq_stream_t stream);
 
 /* ---- decode chain ------------------------------------------------------------------------------
- * n consecutive linears, each computed as fq_linear_w6ax(links[l].x, M, N, K, abits, w_packed, d, ...)
- * in order -- bit-identical outputs -- where links[l].x may lie inside links[l-1].d (a layer's o_proj ->
- * gate_up -> down -> next qkv).  Runs of up to 8 links run as ONE persistent launch when every link's
- * decode plan allows it (M <= 4, N a multiple of 16 and >= 16 x the CU count, x 16-byte aligned) and
- * the run's outputs are disjoint and each x lies either inside the previous link's d (4-byte offset)
- * or outside every output of the run: each linear's weight stream starts before it waits, inside the
- * kernel, for the previous linear's output (read from tagged hand-off granules in the workspace), not
- * behind a kernel boundary.  Other links run as fq_linear_w6ax (xq_buf / xs_buf as
- * there: only links that do not fuse their quantizer use them; workspace as fq_linear_w6ax's).
+ * n consecutive linears, each computed as its entry point would in order -- fq_linear_w6ax (pro 0),
+ * fq_rmsnorm_linear_w6ax (pro 1), fq_silu_linear_w6ax (pro 2); bit-identical outputs and residual
+ * outputs -- where a link's x / in may lie inside the previous link's d and an RMSNorm link's residual
+ * may be an earlier RMSNorm link's res_out (a decoder layer's o_proj -> RMSNorm + gate_up -> SiLU * up +
+ * down_proj -> RMSNorm + next qkv).  Runs of up to 8 links, the first a plain linear, run as ONE
+ * persistent launch when every link's decode plan allows it (M <= 4, N a multiple of 16 and >= 16 x
+ * the CU count, x 16-byte aligned; RMSNorm at M = 1, K = 4096) and no output of the run overlaps
+ * another output or an input except through those hand-offs: each linear's weight stream starts
+ * before it waits, inside the kernel, for its inputs (read from tagged hand-off granules in the chain
+ * workspace), not behind a kernel boundary.  Other links run as their entry points
+ * (xq_buf / xs_buf as there: only links that do not fuse their quantizer use them; workspace as theirs).
  * chain_ws: the chain workspace, 256-byte aligned, fq_chain_workspace_bytes(links, n, M) bytes (a
  * shorter one runs shorter runs or plain linears), zeroed once by fq_chain_workspace_init and then
  * written by chain launches only (one per stream; it may serve every chain of that stream).
@@ -142,10 +144,17 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
  * fq_chain_error_offset() of chain_ws (sticky; results undefined) -- the caller checks it.
  * No FlexQ counterpart: the reference launches one kernel per GEMM call (flexq_gemm_wrapper.cu:99-122). */
 typedef struct fq_chain_link {
-    const uint16_t *x;    /* fp16 [M][K] */
-    const void *w_packed; /* weight image [N][K] */
-    uint16_t *d;          /* fp16 [M][N] */
+    const uint16_t *x;     /* fp16 [M][K]; pro 1: the residual; pro 2: the gate (rows of stride ldh) */
+    const void *w_packed;  /* weight image [N][K] */
+    uint16_t *d;           /* fp16 [M][N] */
     int N, K, abits;
+    int pro;               /* 0: fq_linear_w6ax; 1: fq_rmsnorm_linear_w6ax (M = 1, K = 4096 to chain);
+                              2: fq_silu_linear_w6ax */
+    const uint16_t *in;    /* pro 1: the input added to the residual (or NULL); pro 2: up */
+    const uint16_t *gamma; /* pro 1 */
+    uint16_t *res_out;     /* pro 1 with in: residual + in */
+    float eps;             /* pro 1 */
+    int ldh;               /* pro 2: row stride of gate and up */
 } fq_chain_link;
 fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int M, void *chain_ws, size_t chain_ws_bytes,
                                int8_t *xq_buf, uint16_t *xs_buf, void *workspace, size_t workspace_bytes,

@@ -191,3 +191,106 @@ def test_chain_error_word_fails_fast_and_recovers(ops, dev):
     ops.linear_chain_w6ax(links)
     torch.cuda.synchronize()
     check(ops, links, dev, "after clearing the error word")
+
+
+def _layer_links(ops, dev, g, x_attn, h, n_layers=1):
+    """A LLaMA-2-7B decoder layer's linears after the attention core as chain links (M = 1):
+    o -> RMSNorm(h + o) + gate_up -> SiLU(gate) * up + down -> RMSNorm(h' + down) + next qkv.
+    Returns (links, the same as one callable per link for the sequential reference)."""
+    H, F = 4096, 11008
+    links, x = [], x_attn
+    res = h
+    for _ in range(n_layers):
+        o_out = torch.empty((1, H), dtype=torch.float16, device=dev)
+        gu_out = torch.empty((1, 2 * F), dtype=torch.float16, device=dev)
+        dn_out = torch.empty((1, H), dtype=torch.float16, device=dev)
+        qkv_out = torch.empty((1, 3 * H), dtype=torch.float16, device=dev)
+        r1 = torch.empty((1, H), dtype=torch.float16, device=dev)
+        r2 = torch.empty((1, H), dtype=torch.float16, device=dev)
+        g1 = (1.0 + 0.2 * torch.randn(H, device=dev, generator=g)).half()
+        g2 = (1.0 + 0.2 * torch.randn(H, device=dev, generator=g)).half()
+        links += [(x, image(ops, H, H, g, dev), H, 6, o_out),
+                  ops.chain_rmsnorm(res, g1, image(ops, 2 * F, H, g, dev), 2 * F, 6, gu_out, input=o_out,
+                                    residual_out=r1),
+                  ops.chain_silu(gu_out[:, :F], gu_out[:, F:], image(ops, H, F, g, dev), H, 8, dn_out),
+                  ops.chain_rmsnorm(r1, g2, image(ops, 3 * H, H, g, dev), 3 * H, 6, qkv_out, input=dn_out,
+                                    residual_out=r2)]
+        x, res = qkv_out[:, 2 * H:], r2  # the attention stand-in: ctx = v
+    return links
+
+
+def _sequential_any(ops, links):
+    """Each link through its own entry point, in order, on the same buffers (fresh outputs compared)."""
+    res = []
+    for lk in links:
+        if isinstance(lk, dict) and lk["kind"] == "rmsnorm":
+            out = torch.empty_like(lk["out"])
+            ro = torch.empty_like(lk["residual_out"]) if lk["input"] is not None else None
+            ops.rmsnorm_linear_w6ax(lk["x"], lk["gamma"], lk["w"], lk["N"], lk["abits"], eps=lk["eps"],
+                                    input=lk["input"], residual_out=ro, out=out)
+            res.append((out, ro))
+        elif isinstance(lk, dict):
+            out = torch.empty_like(lk["out"])
+            ops.silu_linear_w6ax(lk["x"], lk["up"], lk["w"], lk["N"], lk["abits"], out=out)
+            res.append((out, None))
+        else:
+            x, wpk, N, abits, o = lk
+            res.append((ops.linear_w6ax(x, wpk, N, abits), None))
+    torch.cuda.synchronize()
+    return res
+
+
+def _outs(lk):
+    if isinstance(lk, dict):
+        return lk["out"], lk.get("residual_out") if lk.get("input") is not None else None
+    return lk[4], None
+
+
+@pytest.mark.parametrize("n_layers", [1, 2])
+def test_chain_decoder_layer_with_producers(ops, dev, n_layers):
+    """o -> RMSNorm + gate_up -> SiLU * up + down -> RMSNorm + qkv as one launch (two layers: 8 links),
+    every output and residual output bit-identical to the four entry points called one by one.  The
+    sequential reference runs AFTER the chain on the chain's own inputs (each link's inputs are the
+    chain's buffers, which the chain filled with the same bits the entry points produce)."""
+    g = torch.Generator(device=dev).manual_seed(41 + n_layers)
+    x_attn = torch.randn((1, 4096), dtype=torch.float16, device=dev, generator=g)
+    h = torch.randn((1, 4096), dtype=torch.float16, device=dev, generator=g)
+    links = _layer_links(ops, dev, g, x_attn, h, n_layers)
+    for rep in range(2):
+        for lk in links:
+            o, ro = _outs(lk)
+            o.fill_(float("nan"))
+            if ro is not None:
+                ro.fill_(float("nan"))
+        ops.linear_chain_w6ax(links)
+        torch.cuda.synchronize()
+        ref = _sequential_any(ops, links)
+        for i, (lk, (ro_ref_out, ro_ref_res)) in enumerate(zip(links, ref)):
+            o, ro = _outs(lk)
+            np.testing.assert_array_equal(o.cpu().numpy().view(np.uint16), ro_ref_out.cpu().numpy().view(np.uint16),
+                                          err_msg=f"rep {rep} link {i} output")
+            if ro is not None:
+                np.testing.assert_array_equal(ro.cpu().numpy().view(np.uint16), ro_ref_res.cpu().numpy().view(np.uint16),
+                                              err_msg=f"rep {rep} link {i} residual output")
+        assert ops.chain_error(dev) == 0
+
+
+def test_chain_silu_link_at_m2(ops, dev):
+    """gate_up -> SiLU * up + down -> qkv at M = 2 (gate / up rows of stride 2F inside the previous
+    output): one launch, bit-identical to the entry points."""
+    g = torch.Generator(device=dev).manual_seed(53)
+    H, F = 4096, 11008
+    x = torch.randn((2, H), dtype=torch.float16, device=dev, generator=g)
+    gu = torch.empty((2, 2 * F), dtype=torch.float16, device=dev)
+    dn = torch.empty((2, H), dtype=torch.float16, device=dev)
+    qkv = torch.empty((2, 3 * H), dtype=torch.float16, device=dev)
+    links = [(x, image(ops, 2 * F, H, g, dev), 2 * F, 6, gu),
+             ops.chain_silu(gu[:, :F], gu[:, F:], image(ops, H, F, g, dev), H, 8, dn),
+             (dn, image(ops, 3 * H, H, g, dev), 3 * H, 6, qkv)]
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    ref = _sequential_any(ops, links)
+    for i, (lk, (r, _)) in enumerate(zip(links, ref)):
+        np.testing.assert_array_equal(_outs(lk)[0].cpu().numpy().view(np.uint16), r.cpu().numpy().view(np.uint16),
+                                      err_msg=f"link {i}")
+    assert ops.chain_error(dev) == 0

@@ -297,3 +297,28 @@ def test_run_layers_fused_producers_llama_width(dev):
             L(h_ref)
         h = run_layers([L, L, L], x.clone())
         assert torch.equal(h.view(torch.int16), h_ref.view(torch.int16)), f"M = {M}"
+
+
+def test_run_layers_chained_bit_identical(dev):
+    """run_layers_chained (decode chains: o -> RMSNorm + gate_up -> SiLU * up + down -> RMSNorm + next
+    qkv as one launch per layer at M = 1; the entry points elsewhere) gives run_layers' bits, at M = 1
+    (chained) and M = 3 (every link alone), over three layers."""
+    from flexq_amd import ops
+    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear, run_layers, run_layers_chained
+    Hs, Fs = 4096, 11008
+    g = torch.Generator().manual_seed(33)
+    rnd = lambda n, k: (torch.randn((n, k), generator=g) / k ** 0.5).half().to(dev)  # noqa: E731
+    lin = lambda n, k, ab=6: W6Linear.from_fp16(rnd(n, k), ab)  # noqa: E731
+    layers = []
+    for _ in range(3):
+        ga = (1 + 0.1 * torch.randn(Hs, generator=g)).half().to(dev)
+        gf = (1 + 0.1 * torch.randn(Hs, generator=g)).half().to(dev)
+        ffn = FlexQFfn(lin(2 * Fs, Hs), lin(Hs, Fs, 8), gf)
+        layers.append(FlexQDecoderLayer(lin(3 * Hs, Hs), lin(Hs, Hs), ffn, ga, lambda qkv: qkv[:, 2 * Hs:]))
+    for M in (1, 3):
+        x = torch.randn((M, Hs), generator=torch.Generator().manual_seed(50 + M)).half().to(dev)
+        h_ref = run_layers(layers, x.clone())
+        h = run_layers_chained(layers, x.clone())
+        torch.cuda.synchronize()
+        assert torch.equal(h.view(torch.int16), h_ref.view(torch.int16)), f"M = {M}"
+        assert ops.chain_error(dev) == 0

@@ -18,6 +18,16 @@ from flexq_amd import ops  # noqa: E402
 
 
 def main():
+    if os.environ.get("FQ_CHAIN_OLDABI"):  # (A/B against a build from before the producer links: plain links only)
+        import ctypes
+
+        class OldLink(ctypes.Structure):
+            _fields_ = [("x", ctypes.c_void_p), ("w_packed", ctypes.c_void_p), ("d", ctypes.c_void_p),
+                        ("N", ctypes.c_int), ("K", ctypes.c_int), ("abits", ctypes.c_int)]
+
+            def __init__(self, x=None, w_packed=None, d=None, N=0, K=0, abits=0, **_kw):
+                super().__init__(x, w_packed, d, N, K, abits)
+        ops._ChainLink = OldLink
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     cfg_name = sys.argv[2] if len(sys.argv) > 2 else "llama2-7b-m1"
     dev = torch.device("cuda", 0)
