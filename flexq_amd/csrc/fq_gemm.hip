@@ -1350,38 +1350,62 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_ke
         asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cb + 4 * k) : "memory");
         return make_uint2(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y));
     };
-    auto ptr = [&](int k) -> uint64_t {
-        const uint2 a = rd2(k);
-        return (uint64_t)a.x | ((uint64_t)a.y << 32);
-    };
     typedef std::conditional_t<CHP, ChainTailP, ChainTailPlain> TAIL;
     constexpr int T0 = FQ_CHAIN_TAIL_OFF / 4, LW = sizeof(LINK) / 4;
     static_assert(T0 % 2 == 0 && LW % 2 == 0 && offsetof(TAIL, n) % 8 == 4, "ds_read_b64 pairs");
     const int n = (int)rd2(T0 + offsetof(TAIL, n) / 4 - 1).y;
-    for (int l = 1; l < n; l++) {
-        const int b = T0 + (l - 1) * LW;
-        ChainLinkP L{};
-        L.x = reinterpret_cast<const uint16_t *>(ptr(b));
-        L.w = reinterpret_cast<const uint32_t *>(ptr(b + 2));
-        L.d = reinterpret_cast<uint16_t *>(ptr(b + 4));
-        L.hx = reinterpret_cast<const uint64_t *>(ptr(b + 6));
-        L.hd = reinterpret_cast<uint64_t *>(ptr(b + 8));
-        constexpr int WO = offsetof(LINK, w0) / 4;
-        if (CHP) {
-            L.in = reinterpret_cast<const uint16_t *>(ptr(b + 10));
-            L.hin = reinterpret_cast<const uint64_t *>(ptr(b + 12));
-            L.gamma = reinterpret_cast<const uint16_t *>(ptr(b + 14));
-            L.res_out = reinterpret_cast<uint16_t *>(ptr(b + 16));
-            L.hr = reinterpret_cast<uint64_t *>(ptr(b + 18));
-            const uint2 a7 = rd2(b + WO + 4);
-            L.eps = __uint_as_float(a7.x);
-            L.ldh_pro = a7.y;
+    // a link's descriptor: its LW / 2 dword pairs read back to back, one wait (a wait per pair cost
+    // ~0.35 us between two linears: seven serial LDS round trips)
+    auto rdlink = [&](int b, uint2 *v) {
+        if constexpr (LW == 14) {
+            asm volatile(
+                "ds_read_b64 %0, %7\n\tds_read_b64 %1, %7 offset:8\n\tds_read_b64 %2, %7 offset:16\n\t"
+                "ds_read_b64 %3, %7 offset:24\n\tds_read_b64 %4, %7 offset:32\n\tds_read_b64 %5, %7 offset:40\n\t"
+                "ds_read_b64 %6, %7 offset:48\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6])
+                : "v"(cb + 4 * b)
+                : "memory");
+        } else {
+            static_assert(LW == 26, "descriptor layouts");
+            asm volatile(
+                "ds_read_b64 %0, %13\n\tds_read_b64 %1, %13 offset:8\n\tds_read_b64 %2, %13 offset:16\n\t"
+                "ds_read_b64 %3, %13 offset:24\n\tds_read_b64 %4, %13 offset:32\n\tds_read_b64 %5, %13 offset:40\n\t"
+                "ds_read_b64 %6, %13 offset:48\n\tds_read_b64 %7, %13 offset:56\n\tds_read_b64 %8, %13 offset:64\n\t"
+                "ds_read_b64 %9, %13 offset:72\n\tds_read_b64 %10, %13 offset:80\n\tds_read_b64 %11, %13 offset:88\n\t"
+                "ds_read_b64 %12, %13 offset:96\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+                  "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12])
+                : "v"(cb + 4 * b)
+                : "memory");
         }
-        const uint2 a5 = rd2(b + WO), a6 = rd2(b + WO + 2);
-        L.w0 = a5.x;
-        L.w1 = a5.y;
-        L.w2 = a6.x;
-        L.w3 = a6.y;
+#pragma unroll
+        for (int k = 0; k < LW / 2; k++)
+            v[k] = make_uint2(__builtin_amdgcn_readfirstlane(v[k].x), __builtin_amdgcn_readfirstlane(v[k].y));
+    };
+    auto p64 = [](uint2 a) -> uint64_t { return (uint64_t)a.x | ((uint64_t)a.y << 32); };
+    for (int l = 1; l < n; l++) {
+        uint2 v[LW / 2];
+        rdlink(T0 + (l - 1) * LW, v);
+        ChainLinkP L{};
+        L.x = reinterpret_cast<const uint16_t *>(p64(v[0]));
+        L.w = reinterpret_cast<const uint32_t *>(p64(v[1]));
+        L.d = reinterpret_cast<uint16_t *>(p64(v[2]));
+        L.hx = reinterpret_cast<const uint64_t *>(p64(v[3]));
+        L.hd = reinterpret_cast<uint64_t *>(p64(v[4]));
+        constexpr int WO = offsetof(LINK, w0) / 8;
+        if constexpr (CHP) {
+            L.in = reinterpret_cast<const uint16_t *>(p64(v[5]));
+            L.hin = reinterpret_cast<const uint64_t *>(p64(v[6]));
+            L.gamma = reinterpret_cast<const uint16_t *>(p64(v[7]));
+            L.res_out = reinterpret_cast<uint16_t *>(p64(v[8]));
+            L.hr = reinterpret_cast<uint64_t *>(p64(v[9]));
+            L.eps = __uint_as_float(v[WO + 2].x);
+            L.ldh_pro = v[WO + 2].y;
+        }
+        L.w0 = v[WO].x;
+        L.w1 = v[WO].y;
+        L.w2 = v[WO + 1].x;
+        L.w3 = v[WO + 1].y;
         chain_link<MT, CHP>(sync, l, L, epoch, DecodePro{});
     }
     if (chain_late(epoch) == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch

@@ -4,7 +4,8 @@ output) in a graph, then reads the per-(WG, linear) wave-0 stamps (s_memrealtime
 start, 1 ring issued, 2 input quantized (after the in-kernel wait), 3 first block landed, 4 stream
 done, 5 linear end.  Prints, per linear, medians and spreads over the WGs (us, from the launch's
 first stamp) and the hand-off: from the last WG's stream end of linear l to each WG's input-ready
-time of linear l + 1."""
+time of linear l + 1.  FQ_STAMPS_PRO=1: the decoder layer's producer chain instead (o -> RMSNorm +
+gate_up -> SiLU * up + down -> RMSNorm + qkv, layers.run_layers_chained's links)."""
 import ctypes
 import os
 import sys
@@ -32,13 +33,25 @@ def main():
     chains = []
     for c in range(6):  # rotating weight sets (cold images, as in the step)
         links, prev = [], x0
+        imgs, outs = [], []
         for (_, N, K, ab) in SHAPES:
             wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
             ws = ((torch.rand((K // 128, N), device=dev, generator=g) + 0.5) / (18.5 * 1.04 * K ** 0.5)).half()
             out = torch.empty((1, N), dtype=torch.float16, device=dev)
             x = prev if prev is x0 else prev.view(-1)[:K].view(1, K)
             links.append((x, ops.pack_w6(wq, ws), N, ab, out))
+            imgs.append(links[-1][1])
+            outs.append(out)
             prev = out
+        if os.environ.get("FQ_STAMPS_PRO"):
+            F = 11008
+            gam = [torch.rand((1, 4096), dtype=torch.float16, device=dev, generator=g) + 0.5 for _ in range(2)]
+            res = [torch.randn((1, 4096), dtype=torch.float16, device=dev, generator=g) for _ in range(3)]
+            gu = outs[1]
+            links = [links[0],
+                     ops.chain_rmsnorm(res[0], gam[0], imgs[1], 22016, 6, gu, input=outs[0], residual_out=res[1]),
+                     ops.chain_silu(gu[:, :F], gu[:, F:], imgs[2], 4096, 6, outs[2]),
+                     ops.chain_rmsnorm(res[1], gam[1], imgs[3], 12288, 6, outs[3], input=outs[2], residual_out=res[2])]
         chains.append(links)
     s = torch.cuda.Stream(dev)
     with torch.cuda.stream(s):
