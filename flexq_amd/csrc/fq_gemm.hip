@@ -42,6 +42,14 @@
 //     no float atomics.  (MI355X_MICROARCH.md "Valid forms", row 1.)
 // =============================================================================================
 
+// decode chain: a producer link waiting for granules loads its ready values behind the ring (0: ahead)
+#ifndef FQ_CHAIN_LATE_READY
+#define FQ_CHAIN_LATE_READY 1
+#endif
+// decode chain: s_sleep between two polls of the hand-off granules
+#ifndef FQ_CHAIN_SLEEP
+#define FQ_CHAIN_SLEEP 1
+#endif
 // cache policy of the weight stream's LDS-DMA (aux: 2 = nt, once-read bytes)
 #ifndef FQ_W_AUX
 #define FQ_W_AUX 2
@@ -669,13 +677,19 @@ __device__ __forceinline__ void decode_body(
     // a ready x's first 16 pairs are loaded ahead of the ring, so they return first.  (Granules are
     // not: a first look at the hand-off ahead of the ring made every linear slower -- the ring issue
     // behind those loads took up to 1.4 us longer)
+    // A producer link that also waits for granules (its `in`) loads its ready values behind the ring
+    // instead: they are not needed before the granules arrive, and ahead of the ring they delay it.
     uint4 xv0[4], gg0 = make_uint4(0, 0, 0, 0);
-    if (CHN && !gr && n > 0) {
+    const bool late = FQ_CHAIN_LATE_READY && CHP && gin;
+    auto ready_loads = [&]() {
+        if (CHN && !gr && n > 0) {
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (4 * u < R) xv0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, chn_off(0, u), 0, 16));
-    }
-    if (CHP && cpro == 1 && n > 0) gg0 = *reinterpret_cast<const uint4 *>(pro.gamma + chn_el(0, 0));  // (RMSNorm: gamma, likewise)
+            for (int u = 0; u < 4; u++)
+                if (4 * u < R) xv0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, chn_off(0, u), 0, 16));
+        }
+        if (CHP && cpro == 1 && n > 0) gg0 = *reinterpret_cast<const uint4 *>(pro.gamma + chn_el(0, 0));  // (RMSNorm: gamma)
+    };
+    if (!late) ready_loads();
     int rit = 0, rj = 0;  // (item, group) of the next block to issue
     auto advance = [&]() {
         if (++rj == ng) {
@@ -696,6 +710,7 @@ __device__ __forceinline__ void decode_body(
     }
     FQ_STAMP(1);
     FQ_CSTAMP(1);
+    if (late) ready_loads();
     // a producer chain's argument block, by wave 0 of linear 0 only, issued behind its ring (needed a
     // linear later; a plain chain's smaller block was loaded as the launch started)
     typedef const uint32_t __attribute__((address_space(4))) kdword;  // (the constant address space)
@@ -742,7 +757,7 @@ __device__ __forceinline__ void decode_body(
                         ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
                     }
                     if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
                     if (spin == (1 << 20) - 1) {
                         failed = true;
                         if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -767,37 +782,42 @@ __device__ __forceinline__ void decode_body(
             uint4 v[4], w[4];  // x (RMSNorm: the residual; SiLU: gate) and `in`
 #pragma unroll
             for (int u = 0; u < 4; u++) w[u] = make_uint4(0, 0, 0, 0);
-            // one pass over both sources: ready values load once, granules until their tags match
+            // both sources: ready values load once, granules until their tags match -- a source whose
+            // tags all matched is not loaded again (the other's re-polls do not queue behind it)
+            bool dx = !gr, din = !gin;
             for (int spin = 0; spin < (1 << 20); spin++) {
-                bool ok = true;
+                bool okx = true, okin = true;
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     if (c + 4 * u >= R) break;
                     const uint32_t el = chn_el(c, u);
                     if (!gr) {
                         if (spin == 0) v[u] = c == 0 ? xv0[u] : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 2, 0, 16));
-                    } else {
+                    } else if (!dx) {
                         const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4, 0, 16));
                         const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4 + 16, 0, 16));
                         v[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
-                        ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                        okx = okx && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
                     }
                     if (hasin && !gin) {
                         if (spin == 0) w[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 2, 0, 16));
-                    } else if (gin) {
+                    } else if (gin && !din) {
                         const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4, 0, 16));
                         const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4 + 16, 0, 16));
                         w[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
-                        ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                        okin = okin && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
                     }
                 }
-                if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
-                __builtin_amdgcn_s_sleep(1);
+                dx = dx || __builtin_amdgcn_ballot_w64(!okx) == 0;  // (wave-uniform)
+                din = din || __builtin_amdgcn_ballot_w64(!okin) == 0;
+                if ((dx && din) || failed) break;
+                __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
                 if (spin == (1 << 20) - 1) {
                     failed = true;
                     if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            FQ_CSTAMP(6);
             if (CHP && cpro == 1) {  // residual add + RMSNorm (M = 1, K = 4 x 128 x NW: lane = chunk 64 wid + lane,
                                   // as the fused producer kernel, PRO 1 above -- the same bits)
                 uint4 r = v[0];
@@ -820,6 +840,7 @@ __device__ __forceinline__ void decode_body(
                 if (lane == 0) ds_write_b32(lds_addr(wsum) + 4 * wid, __float_as_uint(acc));
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
+                FQ_CSTAMP(7);
                 v4i s0 = ds_read_b128(lds_addr(wsum)), s1 = ds_read_b128(lds_addr(wsum) + 16);
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(s0), "+v"(s1)::"memory");
                 float ss = __int_as_float(s0[0]);

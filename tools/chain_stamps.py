@@ -45,7 +45,7 @@ def main():
             prev = out
         if os.environ.get("FQ_STAMPS_PRO"):
             F = 11008
-            gam = [torch.rand((1, 4096), dtype=torch.float16, device=dev, generator=g) + 0.5 for _ in range(2)]
+            gam = [torch.rand((4096,), dtype=torch.float16, device=dev, generator=g) + 0.5 for _ in range(2)]
             res = [torch.randn((1, 4096), dtype=torch.float16, device=dev, generator=g) for _ in range(3)]
             gu = outs[1]
             links = [links[0],
@@ -67,7 +67,7 @@ def main():
     torch.cuda.synchronize()
     st = (ctypes.c_ulonglong * (1024 * NL * NS))()
     assert L.fq_dev_chain_stamps(st, 1024 * NL * NS) == 0
-    a = np.frombuffer(st, dtype=np.uint64).reshape(1024, NL, NS)[:256, :len(SHAPES), :6].astype(np.int64)
+    a = np.frombuffer(st, dtype=np.uint64).reshape(1024, NL, NS)[:256, :len(SHAPES), :8].astype(np.int64)
     t0 = a[:, 0, 0].min()
     us = (a - t0) / 100.0  # 100 MHz -> us
     print("per linear (us from the launch's first stamp): median over WGs [min .. max]")
@@ -83,6 +83,12 @@ def main():
               f"input quantized median {np.median(ready) - last:+.2f} [{ready.min() - last:+.2f} .. {ready.max() - last:+.2f}] us; "
               f"consumer first block {np.median(us[:, li, 3]) - last:+.2f}; ring issued (median) {np.median(us[:, li, 1]) - last:+.2f}")
     print("launch span", f"{us[:, len(SHAPES) - 1, 5].max():.2f} us")
+    if os.environ.get("FQ_STAMPS_PRO"):  # 6: both sources arrived (poll done), 7: RMSNorm's barrier passed
+        for li in range(1, len(SHAPES)):
+            p6, p7 = us[:, li, 6], us[:, li, 7]
+            print(f"{SHAPES[li][0]:8s} ring issued -> poll done {np.median(p6 - us[:, li, 1]):+.2f}  "
+                  f"poll done -> barrier {np.median(p7 - p6) if p7.max() > 0 else float('nan'):+.2f}  "
+                  f"-> quantized {np.median(us[:, li, 2] - (p7 if p7.max() > 0 else p6)):+.2f}")
 
 
 if __name__ == "__main__":

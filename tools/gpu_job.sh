@@ -1,6 +1,6 @@
 # scratch GPU job (development; rewritten per gpurun call)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/chain_stamps.py > gpurun_out/j25_plain.txt 2>&1 || { tail -20 gpurun_out/j25_plain.txt; exit 1; }
-FQ_STAMPS_PRO=1 timeout -k 10 120 python -u tools/chain_stamps.py > gpurun_out/j25_pro.txt 2>&1 || { tail -20 gpurun_out/j25_pro.txt; exit 1; }
-cat gpurun_out/j25_plain.txt gpurun_out/j25_pro.txt | grep -v amdgpu.ids
+for rep in 1 2 3; do for L in flexq_amd/libflexq_hip.so tools/libflexq_hip_sl0.so; do
+  echo "== $L"; FLEXQ_AMD_LIB=$L timeout -k 10 200 python -u tools/chain_bench.py 20 2>&1 | grep -v amdgpu.ids | grep -v "^launches" || exit 1
+done; done
