@@ -111,3 +111,30 @@ def test_fqbmma_instances_exported_with_reference_names():
         assert {n + "_InitFn", n + "_ExecFn"} <= data, n
     funcs = set(re.findall(r"\bT\s+(fq_bmma_op_\w+)", nm.stdout))
     assert {"fq_bmma_op_forget_weight", "fq_bmma_op_device_bytes"} <= funcs
+
+
+def test_chain_host_side():
+    """fq_linear_chain_w6ax's host contract (no GPU calls): the ctypes link struct matches the
+    header's layout, the chain workspace is the sync block plus one hand-off region per link whose
+    output the next link reads (4 B per output element, 256-B rounded) plus one per RMSNorm link with
+    an input (its residual output's granules), and bad arguments are status codes."""
+    from flexq_amd import _lib, ops
+    lib = _lib.load()
+    L = ops._ChainLink
+    assert ctypes.sizeof(L) == 72
+    assert [L.N.offset, L.pro.offset, L.in_.offset, L.gamma.offset, L.eps.offset, L.ldh.offset] == [24, 36, 40, 48, 64, 68]
+    sync = 4096
+    links = (L * 3)()
+    for i, (n, k) in enumerate([(4096, 4096), (22016, 4096), (4096, 11008)]):
+        links[i].N, links[i].K, links[i].abits = n, k, 6
+    assert lib.fq_chain_workspace_bytes(links, 3, 1) == sync + 4096 * 4 + 22016 * 4
+    assert lib.fq_chain_workspace_bytes(links, 3, 3) == sync + 3 * 4096 * 4 + ((3 * 22016 * 4 + 255) // 256) * 256
+    links[1].pro, links[1].in_ = 1, 16  # an RMSNorm link with an input: + its residual's granules
+    assert lib.fq_chain_workspace_bytes(links, 3, 1) == sync + 4096 * 4 + 22016 * 4 + 4096 * 4
+    assert lib.fq_chain_workspace_bytes(links, 1, 1) == sync
+    assert lib.fq_chain_error_offset() == 4 * 32 * 9
+    assert lib.fq_linear_chain_w6ax(None, 1, 1, None, 0, None, None, None, 0, None) == 1  # FQ_ERR_NULL
+    assert lib.fq_linear_chain_w6ax(links, 3, 33, None, 0, None, None, None, 0, None) == 2  # M > 32
+    assert lib.fq_linear_chain_w6ax(links, 3, 1, None, 0, None, None, None, 0, None) == 1  # null x / w / d
+    assert lib.fq_chain_workspace_init(None, 0, None) == 0
+    assert lib.fq_chain_workspace_init(None, 64, None) == 1
