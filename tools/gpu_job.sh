@@ -1,11 +1,5 @@
 # scratch GPU job (development; rewritten per gpurun call)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/f1_tests.txt 2>&1 || { tail -30 gpurun_out/f1_tests.txt; exit 1; }
-tail -2 gpurun_out/f1_tests.txt
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/f1_smoke.txt 2>&1 || { tail -20 gpurun_out/f1_smoke.txt; exit 1; }
-tail -2 gpurun_out/f1_smoke.txt
-timeout -k 10 500 python -u bench.py > gpurun_out/f1_bench.json 2> gpurun_out/f1_bench.err || { tail -30 gpurun_out/f1_bench.err; exit 1; }
-python -c "import json;d=json.loads(open('gpurun_out/f1_bench.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['config'].get('decode_form'),d['decode_chain']['launches_ms_per_step']);print('c3',d['c3_llama2_7b_m16']['ms_per_step'],'c5',d['c5_llama3_8b_prefill']['ms_per_step'],'e2e',d['decoder_layers_e2e']['M1']['w6_ms_per_step'])"
-bash tools/profile_round.sh r04 > gpurun_out/f1_prof.log 2>&1 || { tail -20 gpurun_out/f1_prof.log; exit 1; }
-tail -3 gpurun_out/f1_prof.log
+timeout -k 10 900 python -u bench.py --gpus 2 --share-gpu --steps 3 --warmup 1 --cpu-budget 0 --no-fp16-compare --no-reference-sweep > gpurun_out/f2_share2.json 2> gpurun_out/f2_share2.err || { tail -30 gpurun_out/f2_share2.err; exit 1; }
+python -c "import json;d=json.loads(open('gpurun_out/f2_share2.json').read().strip().splitlines()[-1]);print(d['value'],d['n_gpus'],d['ms_per_step'],d['config'].get('parallelism'),d.get('rehearsal'));print(list(d.keys()))"
