@@ -178,6 +178,24 @@ def run_step(stack, M, world, group=None, gather=True, staged=False):
                 dist.all_gather_into_tensor(p["full"], p["out"].view(-1), group=group)
 
 
+def run_step_qo(stack, M):
+    """The prefill step with each linear's activation quantize moved into the previous GEMM's
+    epilogue (ops.gemm_w6ax_q, fq_gemm_w6ax_u8_q): the first input is quantized by its own launch,
+    every later one by the GEMM that produces it -- the same codes as run_step's separate quantize
+    launches (each linear's input is the leading M x K values of the previous output)."""
+    lins_ = linears(stack)
+    p0 = lins_[0][1]
+    xq, xs = ops.quantize_act(p0["x"], p0["abits"])
+    for i, (_, p) in enumerate(lins_):
+        if i + 1 < len(lins_):
+            nx = lins_[i + 1][1]
+            assert nx["x"].data_ptr() == p["out"].data_ptr() and tuple(nx["x"].shape) == (M, nx["K"])
+            _, xq, xs = ops.gemm_w6ax_q(xq, xs, p["pk"], p["Nl"], p["abits"], p["w_u8"], (M, nx["K"]), nx["abits"],
+                                        out=p["out"])
+        else:
+            ops.gemm_w6ax(xq, xs, p["pk"], p["Nl"], p["abits"], out=p["out"], w_u8=p["w_u8"])
+
+
 def chain_runs(stack):
     """The step's linears as decode chains (fq_linear_chain_w6ax), cut where the model's attention core
     sits: qkv_0 | o_0, gate_up_0, down_0, qkv_1 | o_1, ... -- the attention (out of scope) is a kernel of
@@ -657,6 +675,23 @@ def measure_single(ctx, name, merge, steps, warmup):
             elapsed, ev_s = el_c, ev_c
             chain["taken"] = True
         del replay_c
+    qo = None
+    if M >= ops.PREFILL_U8_MIN_M and not ctx.a.no_qo:  # quantize in the producer's epilogue (same codes)
+        last_out = linears(stack)[-1][1]["out"]
+        ref = last_out.clone()
+        replay_q = ctx.prepare(lambda: run_step_qo(stack, M), not ctx.a.no_graph)
+        el_q, ev_q = ctx.timed(replay_q, steps, warmup)
+        same = bool(torch.equal(last_out.view(torch.int16), ref.view(torch.int16)))
+        del ref
+        qo = {"what": "each linear's activation quantize in the previous prefill GEMM's epilogue "
+                      "(fq_gemm_w6ax_u8_q; the step's first input quantized by its own launch)",
+              "ms_per_step": round(el_q / steps * 1e3, 4),
+              "separate_quantize_ms_per_step": round(elapsed / steps * 1e3, 4),
+              "last_output_identical": same}
+        if same and el_q < elapsed:
+            elapsed, ev_s = el_q, ev_q
+            qo["taken"] = True
+        del replay_q
     flops_step = layers * sum(2.0 * M * N * K for (_, N, K, _) in lins)
     out = {"what": f"BASELINE config: {desc}, the dependent linear stack of every layer, one HIP graph" +
                    (" (weights: the fq6 image + its int8 MFMA operands unpacked once at load, "
@@ -668,6 +703,8 @@ def measure_single(ctx, name, merge, steps, warmup):
            "finite": bool(torch.isfinite(linears(stack)[-1][1]["out"].float()).all().item())}
     if chain is not None:
         out["decode_chain"] = chain
+    if qo is not None:
+        out["epilogue_quantize"] = qo
     if M > PREFILL_M:
         codes = {}
         for nm, p in linears(stack):
@@ -859,6 +896,8 @@ def main():
                     help="N = 1: skip the reference's kernel sweep (engine/test_flexq_kernel.sh, README.md:189's form)")
     ap.add_argument("--no-layers", action="store_true",
                     help="skip the end-to-end decoder-layer comparison against fp16 (M = 1 and 16)")
+    ap.add_argument("--no-qo", action="store_true",
+                    help="prefill steps: skip the form with each quantize in the previous GEMM's epilogue")
     ap.add_argument("--no-chain", action="store_true",
                     help="N = 1 decode: time only one launch per linear (default: also the decode chains, "
                          "fq_linear_chain_w6ax, taken for `value` when bit-identical and faster)")

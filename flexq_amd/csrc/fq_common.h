@@ -91,6 +91,33 @@ __device__ __forceinline__ int cvt_i32_sat(float v) {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// A group's scale from its absmax mx (a non-negative fp16 value, as fp32), and the element step's
+// reciprocal rcb.  IEEE fp32 absmax / hi as a Newton-corrected product with y = RN(1/hi):
+// bit-identical over every fp16 absmax (exhaustive: tests/test_oracle.py::
+// test_quantizer_division_by_constant_is_exact).
+// Element step: roundf(RN(x / r)) == trunc(RN(x * rcb + copysign(0.5, x))) with
+// rcb = RN(v_rcp(r) * (1 + 2^-20)), one fused multiply-add per element.  x and r are fp16,
+// so a quotient that is not an exact tie k + 0.5 lies far beyond the reciprocal's error from
+// one, and the 2^-20 bias carries an exact tie across the truncation boundary.  Exhaustive
+// over every fp16 absmax and element, both bit widths, the reciprocal off by up to 4 ulp
+// (oracle/fq_oracle.c fqo_check_quant_fma, tests/test_oracle.py).  r = 0 (an all-zero group)
+// gives 0 * inf = NaN and r = inf gives +-0.5: code 0, as the IEEE quotient's class does; the
+// truncating, saturating v_cvt_i32_f32 maps NaN to 0 and +-inf to the int range.
+__device__ __forceinline__ uint16_t quant_scale(float mx, int bits, float &rcb) {
+    const int hi = (1 << (bits - 1)) - 1;
+    const float fhi = (float)hi, y = bits == 8 ? (float)(1.0 / 127.0) : (float)(1.0 / 31.0);
+    const float m1 = mx * y;
+    const float maxv = __builtin_isfinite(m1) ? fmaf(fmaf(-m1, fhi, mx), y, m1) : m1;
+    const uint16_t sh = f2h(maxv);
+    rcb = __builtin_amdgcn_rcpf(h2f(sh)) * (1.0f + 0x1p-20f);
+    return sh;
+}
+
+// The element step (above) for one fp16 value x (as fp32): its code, clamped to [lo, hi].
+__device__ __forceinline__ int quant_code(float x, float rcb, int lo, int hi) {
+    return med3_i32(cvt_i32_sat(fmaf(x, rcb, __builtin_copysignf(0.5f, x))), lo, hi);
+}
+
 // One (row, 128-group) per 16 lanes, 8 fp16 values per lane: absmax over the values converted to
 // fp32 (fmaxf skips NaN, as the reference's __hmax), the element step on the converted values.
 // (An integer-absmax variant -- a packed-u16 max over the fp16 bit patterns, one conversion instead
@@ -107,22 +134,8 @@ __device__ __forceinline__ uint16_t quant_group16(uint4 raw, int bits, uint2 &co
         mx = fmaxf(mx, fmaxf(fabsf(v[i].x), fabsf(v[i].y)));
     }
     mx = max16_nonneg(mx);
-    // IEEE fp32 absmax / hi as a Newton-corrected product with y = RN(1/hi): bit-identical over
-    // every fp16 absmax (exhaustive: tests/test_oracle.py::test_quantizer_division_by_constant_is_exact)
-    const float fhi = (float)hi, y = bits == 8 ? (float)(1.0 / 127.0) : (float)(1.0 / 31.0);
-    const float m1 = mx * y;
-    const float maxv = __builtin_isfinite(m1) ? fmaf(fmaf(-m1, fhi, mx), y, m1) : m1;
-    const uint16_t sh = f2h(maxv);
-    const float r = h2f(sh);
-    // Element step: roundf(RN(x / r)) == trunc(RN(x * rcb + copysign(0.5, x))) with
-    // rcb = RN(v_rcp(r) * (1 + 2^-20)), one fused multiply-add per element.  x and r are fp16,
-    // so a quotient that is not an exact tie k + 0.5 lies far beyond the reciprocal's error from
-    // one, and the 2^-20 bias carries an exact tie across the truncation boundary.  Exhaustive
-    // over every fp16 absmax and element, both bit widths, the reciprocal off by up to 4 ulp
-    // (oracle/fq_oracle.c fqo_check_quant_fma, tests/test_oracle.py).  r = 0 (an all-zero group)
-    // gives 0 * inf = NaN and r = inf gives +-0.5: code 0, as the IEEE quotient's class does; the
-    // truncating, saturating v_cvt_i32_f32 maps NaN to 0 and +-inf to the int range.
-    const float rcb = __builtin_amdgcn_rcpf(r) * (1.0f + 0x1p-20f);
+    float rcb;
+    const uint16_t sh = quant_scale(mx, bits, rcb);
     const v2f rcb2 = {rcb, rcb};
     int c[8];
 #pragma unroll

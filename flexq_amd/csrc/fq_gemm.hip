@@ -1865,10 +1865,17 @@ __device__ unsigned long long g_pb_stamps[256 * PB_WAVES * 4];
 // ABL: development ablations as in fq_gemm_prefill_kernel (1, 2, 4, 8, 16; 32 stamps).  XSF (M % 256 == 0:
 // every row tile full, its x-scales 16-byte aligned): the 256 x-scales of a group arrive packed in
 // one 512-byte DMA piece instead of four 64-lane ushort pieces into dword slots.
-template <bool DBG, int ABL = 0, bool XSF = false>
+// QO: the epilogue also quantizes the fp16 output for the next linear (PbQ; N % 128 == 0): a tile
+// row's 256 columns are two whole 128-column groups, each held by a pair of waves (wn 0-1, 2-3).
+struct PbQ {
+    int8_t *qx;    // int8 [qM][qK]: the output's leading qM * qK values, read row-major as qM x qK
+    uint16_t *qs;  // fp16 [qK / 128][qM]
+    int qM, qK, qbits;
+};
+template <bool DBG, int ABL = 0, bool XSF = false, bool QO = false>
 __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk, int M,
-    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu) {
+    int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg, const char *__restrict__ wu, PbQ qo) {
     extern __shared__ __attribute__((aligned(16))) char pb_smem[];
     char *sa = pb_smem, *sbu = pb_smem + 2 * PB_ASTAGE;
     const int G = K / FQ_GROUP, NT = (N + 15) / 16;
@@ -2109,6 +2116,69 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                         if (n + r < N) dst[r] = (uint16_t)(pk[r >> 2][(r >> 1) & 1] >> (16 * (r & 1)));
                 }
             }
+        }
+    }
+    if constexpr (QO) {
+        // The next linear's activation codes, as fq_quantize_act computes them from the fp16 output:
+        // per (row, 128-column group) the absmax of the fp16 values -- this lane's 16 (4 blocks x 4
+        // columns), the row's 4 lanes (lane ^ 16, ^ 32), then the partner wave's half through LDS
+        // (the stage buffers are idle: every wave is past its last fragment read and DMA wait) --
+        // then quant_scale / quant_code on each value.
+        const int hi = (1 << (qo.qbits - 1)) - 1, lo = -(1 << (qo.qbits - 1));
+        float *amx = reinterpret_cast<float *>(pb_smem);  // [wave][mi][16 rows]
+        float mx[8];
+#pragma unroll
+        for (int mi = 0; mi < 8; mi++) {
+            float m = -1.0f;  // (the reference's seed; fmaxf skips NaN)
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) m = fmaxf(m, fabsf(h2f(f2h(out[mi][ni][r] * 0.25f))));
+            m = fmaxf(m, __shfl_xor(m, 16));
+            mx[mi] = fmaxf(m, __shfl_xor(m, 32));
+        }
+        __syncthreads();
+        if (lane < 16) {
+#pragma unroll
+            for (int mi = 0; mi < 8; mi++) amx[(wid * 8 + mi) * 16 + lane] = mx[mi];
+        }
+        __syncthreads();
+        const size_t lim = (size_t)qo.qM * qo.qK;
+        const int gcol = t0 * 16 + (wn >> 1) * FQ_GROUP;  // the group's first column
+#pragma unroll
+        for (int mi = 0; mi < 8; mi++) {
+            const int m = m0 + arow + mi * 16;
+            const float gm = fmaxf(mx[mi], amx[((wid ^ 1) * 8 + mi) * 16 + (lane & 15)]);
+            float rcb;
+            const uint16_t sh = quant_scale(gm, qo.qbits, rcb);
+            const size_t f0 = (size_t)m * N + gcol;  // the group's flat index
+            if (m >= M || gcol >= N || f0 >= lim) continue;
+            if (lane < 16 && (wn & 1) == 0)
+                qo.qs[(f0 % qo.qK) / FQ_GROUP * (size_t)qo.qM + f0 / qo.qK] = sh;
+            uint32_t w[4];  // block ni's 4 codes of this lane's columns 16 ni + 4 h ..
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++) {
+                w[ni] = 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                    w[ni] |= ((uint32_t)quant_code(h2f(f2h(out[mi][ni][r] * 0.25f)), rcb, lo, hi) & 0xffu) << (8 * r);
+            }
+            // 4 x 4 transpose over (16-lane row h, block ni): permlane32 swaps, then permlane16 swaps
+            // leave row h with block h's 16 consecutive codes -- one 16-byte store instead of four
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const auto t = __builtin_amdgcn_permlane32_swap(w[k], w[k + 2], false, false);
+                w[k] = t[0];
+                w[k + 2] = t[1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k += 2) {
+                const auto t = __builtin_amdgcn_permlane16_swap(w[k], w[k + 1], false, false);
+                w[k] = t[0];
+                w[k + 1] = t[1];
+            }
+            const int n = (t0 + wn * 4 + (lane >> 4)) * 16;
+            *reinterpret_cast<uint4 *>(qo.qx + (size_t)m * N + n) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
 }
@@ -2814,7 +2884,7 @@ extern "C" fq_status fq_gemm_w6ax(const int8_t *xq, const uint16_t *xs, const vo
 // fq_unpack_w8_kernel): the 256 x 256 tile kernel, or the 128 x 128 one when its last-round fill is
 // better (M >= PF_U8_MIN_M).
 static fq_status launch_prefill_u8(const int8_t *xq, const uint16_t *xs, const void *w_packed, const char *wu, int M,
-                                   int N, int K, uint16_t *d, int32_t *acc_dbg, hipStream_t s) {
+                                   int N, int K, uint16_t *d, int32_t *acc_dbg, hipStream_t s, const PbQ *q = nullptr) {
     const int NT = (N + 15) / 16;
     const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
     const unsigned nbig = (unsigned)(((M + PB_BM - 1) / PB_BM) * ((NT + PB_TILES - 1) / PB_TILES));
@@ -2839,15 +2909,19 @@ static fq_status launch_prefill_u8(const int8_t *xq, const uint16_t *xs, const v
             hipLaunchKernelGGL((fq_gemm_prefill_kernel<false, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,
                                xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, 1, nullptr);
         FQ_LAUNCH_CHECK();
+        // (the 128 x 128 tile holds one group per row only across two WGs: its output is quantized apart)
+        if (q) return fq_quantize_act(d, q->qM, q->qK, q->qbits, q->qx, q->qs, s);
         return FQ_OK;
     }
-#define FQ_BIG(dbg, xf)                                                                                  \
-    hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
-                       xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu)
+#define FQ_BIG(dbg, xf, qo)                                                                                  \
+    hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<dbg, 0, xf, qo>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
+                       xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, qo ? *q : PbQ{})
     if (acc_dbg) {
-        if (xsf) FQ_BIG(true, true); else FQ_BIG(true, false);
+        if (xsf) FQ_BIG(true, true, false); else FQ_BIG(true, false, false);
+    } else if (q) {
+        if (xsf) FQ_BIG(false, true, true); else FQ_BIG(false, false, true);
     } else {
-        if (xsf) FQ_BIG(false, true); else FQ_BIG(false, false);
+        if (xsf) FQ_BIG(false, true, false); else FQ_BIG(false, false, false);
     }
 #undef FQ_BIG
     FQ_LAUNCH_CHECK();
@@ -2910,7 +2984,7 @@ fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_
 #define FQ_BABL(v)                                                                                         \
         if (abl == v)                                                                                        \
             hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<false, v>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
-                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu);
+                               xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, PbQ{});
         FQ_BABL(1) FQ_BABL(2) FQ_BABL(3) FQ_BABL(4) FQ_BABL(8) FQ_BABL(12) FQ_BABL(16) FQ_BABL(7) FQ_BABL(15) FQ_BABL(32)
 #undef FQ_BABL
         FQ_LAUNCH_CHECK();
@@ -2982,6 +3056,27 @@ extern "C" fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const
     const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
     if (nwg > 0x7fffffffL) return FQ_ERR_SHAPE;
     return launch_prefill_u8(xq, xs, w_packed, (const char *)w_u8, M, N, K, d, acc_dbg, (hipStream_t)stream);
+}
+
+extern "C" fq_status fq_gemm_w6ax_u8_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8,
+                                       int M, int N, int K, int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM,
+                                       int qK, int qbits, void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+    if (!qxq || !qxs) return FQ_ERR_NULL;
+    if (qM <= 0 || qK <= 0 || qK % FQ_GROUP || (size_t)qM * qK > (size_t)M * N) return FQ_ERR_SHAPE;
+    if (qbits != 6 && qbits != 8) return FQ_ERR_BITS;
+    if (M < PF_U8_MIN_M || N % FQ_GROUP) {  // (no epilogue form: the GEMM, then the quantizer -- the same bits)
+        const fq_status st = fq_gemm_w6ax_u8(xq, xs, w_packed, w_u8, M, N, K, abits, d, nullptr, workspace,
+                                             workspace_bytes, stream);
+        return st != FQ_OK ? st : fq_quantize_act(d, qM, qK, qbits, qxq, qxs, stream);
+    }
+    if (!xq || !xs || !w_packed || !w_u8 || !d) return FQ_ERR_NULL;
+    if (K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    const int NT = (N + 15) / 16;
+    const long nwg = (long)((M + PF_BM - 1) / PF_BM) * ((NT + PF_TILES - 1) / PF_TILES);
+    if (nwg > 0x7fffffffL || (size_t)M * N >= ((size_t)1 << 40)) return FQ_ERR_SHAPE;
+    const PbQ q = {qxq, qxs, qM, qK, qbits};
+    return launch_prefill_u8(xq, xs, w_packed, (const char *)w_u8, M, N, K, d, nullptr, (hipStream_t)stream, &q);
 }
 
 extern "C" fq_status fq_gather_wait(const fq_gather *gather, uint32_t *err, fq_stream_t stream) {

@@ -225,6 +225,40 @@ def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None, w_u8=None):
     return (out, acc) if return_acc else out
 
 
+def gemm_w6ax_q(xq, xs, wpk, N, abits, w_u8, q_shape, qbits, out=None):
+    """gemm_w6ax over prepared operands (w_u8, prefill sizes) that also returns the NEXT linear's
+    quantized input (fq_gemm_w6ax_u8_q): the fp16 output's leading qM * qK values read row-major as
+    [qM, qK] and quantized to qbits -- bit-identical to quantize_act(out.view(-1)[:qM*qK].view(qM, qK),
+    qbits), computed in the 256 x 256 prefill kernel's epilogue.  Returns (out, qxq, qxs)."""
+    _dev(xq, torch.int8, "xq", 2)
+    M, K = xq.shape
+    _k_ok(K)
+    _dev(xs, torch.float16, "xs", 2)
+    _need(tuple(xs.shape) == (K // GROUP, M), f"xs must be [K/128, M] = {(K // GROUP, M)}")
+    _img_ok(wpk, N, K)
+    _need(abits in (6, 8) and qbits in (6, 8), "abits and qbits must be 6 or 8")
+    qM, qK = q_shape
+    _k_ok(qK)
+    _need(0 < qM * qK <= M * N, "the next input must be a prefix of the output")
+    dev = xq.device
+    _dev(w_u8, torch.uint8, "w_u8", 1)
+    _need(w_u8.numel() >= int(_lib.load().fq_prefill_weight_bytes(N, K)) and w_u8.device == dev,
+          "w_u8 must be prepare_prefill_weights(wpk, N, K) on the operands' device")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float16, device=dev)
+    else:
+        _dev(out, torch.float16, "out", 2)
+        _need(tuple(out.shape) == (M, N), "out shape mismatch")
+    qxq = torch.empty((qM, qK), dtype=torch.int8, device=dev)
+    qxs = torch.empty((qK // GROUP, qM), dtype=torch.float16, device=dev)
+    s = _stream(xq)
+    nb = gemm_workspace_bytes(M, N, K)
+    wbuf = workspace(dev, nb, s.value)
+    _lib.call("fq_gemm_w6ax_u8_q", _ptr(xq), _ptr(xs), _ptr(wpk), _ptr(w_u8), M, N, K, abits, _ptr(out), _ptr(qxq),
+              _ptr(qxs), qM, qK, qbits, _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    return out, qxq, qxs
+
+
 def linear_w6ax(x, wpk, N, abits=6, out=None, w_u8=None):
     """Quantize + GEMM (FLEXQGEMMWrapper::gemm(const half* A ...)) for fp16 x [M,K].  w_u8: the
     prepared operands of prepare_prefill_weights (prefill sizes: quantize + fq_gemm_w6ax_u8)."""

@@ -176,6 +176,16 @@ fq_status fq_prefill_unpack_weights(const void *w_packed, int N, int K, void *w_
 fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8, int M,
                           int N, int K, int abits, uint16_t *d, int32_t *acc_dbg, void *workspace,
                           size_t workspace_bytes, fq_stream_t stream);
+/* fq_gemm_w6ax_u8 that also emits the NEXT linear's quantized input: d's leading qM * qK values,
+ * read row-major as a [qM][qK] activation (qK % 128 == 0, qM * qK <= M * N), quantized to qbits
+ * into qxq (int8 [qM][qK]) and qxs (fp16 [qK/128][qM]) -- bit-identical to
+ * fq_quantize_act(d, qM, qK, qbits, qxq, qxs) after the GEMM.  With N % 128 == 0 on the 256 x 256
+ * prefill tiles it runs in the GEMM's epilogue (a tile row holds two whole 128-column groups), so no
+ * separate quantize pass reads d back; otherwise it is the GEMM, then fq_quantize_act.  The reference
+ * quantizes every GEMM input in its own packing kernel (flexq_gemm_wrapper.cu:99-122). */
+fq_status fq_gemm_w6ax_u8_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8, int M,
+                            int N, int K, int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM, int qK,
+                            int qbits, void *workspace, size_t workspace_bytes, fq_stream_t stream);
 
 /* ---- fused producers of the activation codes ---------------------------- */
 /* Residual add + RMSNorm (T5 / LLaMA style: no mean, no bias) + dynamic group quantization, one

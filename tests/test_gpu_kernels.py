@@ -620,6 +620,34 @@ def test_prefill_resident_weights_bit_identical(ops, dev, M, N, K):
     assert torch.equal(y1.view(torch.int16), y2.view(torch.int16))
 
 
+@pytest.mark.parametrize("M,N,K,qM,qK,qbits", [
+    (8192, 6144, 1024, 8192, 4096, 8),     # qkv -> o: the next input a prefix of the output (256 x 256 epilogue)
+    (4096, 28672, 1024, 8192, 14336, 8),   # gate_up -> down shape: the next rows straddle the output rows
+    (4096, 4096, 1024, 4096, 4096, 6),     # A6 codes
+    (2048, 4096, 1024, 2048, 4096, 8),     # 128 x 128 tiles (fill rule): the GEMM, then the quantizer
+    (2048, 1000, 1280, 3200, 640, 8),      # N % 128 != 0: the GEMM, then the quantizer
+    (32, 4096, 4096, 32, 4096, 8),         # decode sizes: the same
+])
+def test_prefill_quantized_output_bit_identical(ops, dev, M, N, K, qM, qK, qbits):
+    """fq_gemm_w6ax_u8_q: the next linear's codes and scales from the prefill GEMM's epilogue are
+    bit-identical to fq_quantize_act over the fp16 output's leading qM x qK values, and the fp16
+    output is the plain GEMM's."""
+    g = torch.Generator(device=dev).manual_seed(M + 5 * N + qK)
+    xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    w_u8 = ops.prepare_prefill_weights(pk, N, K)
+    d0 = ops.gemm_w6ax(xq, xs, pk, N, 8, w_u8=w_u8)
+    d1, qxq, qxs = ops.gemm_w6ax_q(xq, xs, pk, N, 8, w_u8, (qM, qK), qbits)
+    rq, rs = ops.quantize_act(d1.view(-1)[:qM * qK].view(qM, qK), qbits)
+    torch.cuda.synchronize()
+    assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+    assert torch.equal(qxs.view(torch.int16), rs.view(torch.int16))
+    assert torch.equal(qxq, rq)
+
+
 # The round-1 prefill kernel with VGPR-destination asm loads faulted on one shape of this list
 # (not recorded which; DESIGN.md §4.2): every shape of that list stays here as the regression set.
 @pytest.mark.parametrize("M,N,K,abits,with_acc", [
