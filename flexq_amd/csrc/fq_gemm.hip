@@ -2126,14 +2126,18 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
         // then quant_scale / quant_code on each value.
         const int hi = (1 << (qo.qbits - 1)) - 1, lo = -(1 << (qo.qbits - 1));
         float *amx = reinterpret_cast<float *>(pb_smem);  // [wave][mi][16 rows]
+        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+        auto halves = [&](int mi, int ni, int k) {  // the output's fp16 values of columns 16 ni + 4 h + 2k, +1
+            return __builtin_bit_cast(h2v, pack_h2(out[mi][ni][2 * k] * 0.25f, out[mi][ni][2 * k + 1] * 0.25f));
+        };
         float mx[8];
 #pragma unroll
         for (int mi = 0; mi < 8; mi++) {
-            float m = -1.0f;  // (the reference's seed; fmaxf skips NaN)
+            // packed |.| max (v_pk_max_f16: maxNum skips NaN, as fmaxf) over the lane's 16 values
+            h2v a = __builtin_elementwise_abs(halves(mi, 0, 0));
 #pragma unroll
-            for (int ni = 0; ni < 4; ni++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) m = fmaxf(m, fabsf(h2f(f2h(out[mi][ni][r] * 0.25f))));
+            for (int j = 1; j < 8; j++) a = __builtin_elementwise_max(a, __builtin_elementwise_abs(halves(mi, j >> 1, j & 1)));
+            float m = fmaxf(-1.0f, fmaxf((float)a.x, (float)a.y));  // (the reference's seed -1)
             m = fmaxf(m, __shfl_xor(m, 16));
             mx[mi] = fmaxf(m, __shfl_xor(m, 32));
         }
@@ -2158,10 +2162,19 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
             uint32_t w[4];  // block ni's 4 codes of this lane's columns 16 ni + 4 h ..
 #pragma unroll
             for (int ni = 0; ni < 4; ni++) {
-                w[ni] = 0;
+                int c[4];
 #pragma unroll
-                for (int r = 0; r < 4; r++)
-                    w[ni] |= ((uint32_t)quant_code(h2f(f2h(out[mi][ni][r] * 0.25f)), rcb, lo, hi) & 0xffu) << (8 * r);
+                for (int k = 0; k < 2; k++) {  // the element step on the fp16 values (v_fma_mix_f32)
+                    const h2v v = halves(mi, ni, k);
+                    const uint32_t b = __builtin_bit_cast(uint32_t, v);
+                    const float hs0 = __uint_as_float(((b << 16) & 0x80000000u) | 0x3f000000u);  // copysign(0.5, x)
+                    const float hs1 = __uint_as_float((b & 0x80000000u) | 0x3f000000u);
+                    c[2 * k] = med3_i32(cvt_i32_sat(fmaf((float)v.x, rcb, hs0)), lo, hi);
+                    c[2 * k + 1] = med3_i32(cvt_i32_sat(fmaf((float)v.y, rcb, hs1)), lo, hi);
+                }
+                const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)c[1], (uint32_t)c[0], 0x0c0c0400u);
+                const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)c[3], (uint32_t)c[2], 0x0c0c0400u);
+                w[ni] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
             }
             // 4 x 4 transpose over (16-lane row h, block ni): permlane32 swaps, then permlane16 swaps
             // leave row h with block h's 16 consecutive codes -- one 16-byte store instead of four
