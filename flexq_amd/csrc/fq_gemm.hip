@@ -3077,6 +3077,13 @@ extern "C" fq_status fq_gemm_w6ax_u8_q(const int8_t *xq, const uint16_t *xs, con
     if (!qxq || !qxs) return FQ_ERR_NULL;
     if (qM <= 0 || qK <= 0 || qK % FQ_GROUP || (size_t)qM * qK > (size_t)M * N) return FQ_ERR_SHAPE;
     if (qbits != 6 && qbits != 8) return FQ_ERR_BITS;
+    // the next input's buffers are written while other workgroups still read the operands: no overlap
+    const size_t qb = (size_t)qM * qK, qsb = (size_t)(qK / FQ_GROUP) * qM * 2, db = (size_t)M * N * 2;
+    if (ranges_overlap(qxq, qb, xq, (size_t)M * K) || ranges_overlap(qxq, qb, xs, (size_t)(K / FQ_GROUP) * M * 2) ||
+        ranges_overlap(qxq, qb, d, db) || ranges_overlap(qxs, qsb, xq, (size_t)M * K) ||
+        ranges_overlap(qxs, qsb, xs, (size_t)(K / FQ_GROUP) * M * 2) || ranges_overlap(qxs, qsb, d, db) ||
+        ranges_overlap(qxq, qb, qxs, qsb))
+        return FQ_ERR_SHAPE;
     if (M < PF_U8_MIN_M || N % FQ_GROUP) {  // (no epilogue form: the GEMM, then the quantizer -- the same bits)
         const fq_status st = fq_gemm_w6ax_u8(xq, xs, w_packed, w_u8, M, N, K, abits, d, nullptr, workspace,
                                              workspace_bytes, stream);

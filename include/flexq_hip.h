@@ -179,7 +179,8 @@ fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const void *w_pa
 /* fq_gemm_w6ax_u8 that also emits the NEXT linear's quantized input: d's leading qM * qK values,
  * read row-major as a [qM][qK] activation (qK % 128 == 0, qM * qK <= M * N), quantized to qbits
  * into qxq (int8 [qM][qK]) and qxs (fp16 [qK/128][qM]) -- bit-identical to
- * fq_quantize_act(d, qM, qK, qbits, qxq, qxs) after the GEMM.  With N % 128 == 0 on the 256 x 256
+ * fq_quantize_act(d, qM, qK, qbits, qxq, qxs) after the GEMM; qxq and qxs may not overlap xq, xs, d
+ * or each other (FQ_ERR_SHAPE).  With N % 128 == 0 on the 256 x 256
  * prefill tiles it runs in the GEMM's epilogue (a tile row holds two whole 128-column groups), so no
  * separate quantize pass reads d back; otherwise it is the GEMM, then fq_quantize_act.  The reference
  * quantizes every GEMM input in its own packing kernel (flexq_gemm_wrapper.cu:99-122). */

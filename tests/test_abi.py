@@ -138,3 +138,23 @@ def test_chain_host_side():
     assert lib.fq_linear_chain_w6ax(links, 3, 1, None, 0, None, None, None, 0, None) == 1  # null x / w / d
     assert lib.fq_chain_workspace_init(None, 0, None) == 0
     assert lib.fq_chain_workspace_init(None, 64, None) == 1
+
+
+def test_prefill_quantized_output_host_checks():
+    """fq_gemm_w6ax_u8_q's host-side validation (no GPU calls): null next-input buffers, a next
+    input that is not a prefix of the output or has K % 128 != 0, bad bits, and next-input buffers
+    overlapping the operands or the output are status codes."""
+    from flexq_amd import _lib
+    lib = _lib.load()
+    P = ctypes.c_void_p
+    M, N, K = 4096, 4096, 4096
+    xq, xs, w, wu, d = P(1 << 32), P(2 << 32), P(3 << 32), P(4 << 32), P(5 << 32)
+    qx, qs = P(6 << 32), P(7 << 32)
+    call = lambda qxq, qxs, qM, qK, qb: lib.fq_gemm_w6ax_u8_q(xq, xs, w, wu, M, N, K, 8, d, qxq, qxs, qM, qK, qb,  # noqa: E731
+                                                                None, 0, None)
+    assert call(None, qs, M, K, 8) == 1
+    assert call(qx, qs, M, 100, 8) == 2
+    assert call(qx, qs, 2 * M, N, 8) == 2          # more than the output holds
+    assert call(qx, qs, M, K, 7) == 3
+    assert call(xq, qs, M, K, 8) == 2              # codes over the operand codes
+    assert call(qx, P(5 << 32), M, K, 8) == 2      # scales over the output
