@@ -78,6 +78,11 @@ def alg_read_bytes(M, N, K, abits, fused=True):
     return alg_bytes(M, N, K, abits, fused) - 2 * M * N
 
 
+def fp16_bytes(M, N, K):
+    """HBM bytes of one fp16 F.linear: the fp16 weight, the fp16 input and output."""
+    return 2 * N * K + 2 * M * K + 2 * M * N
+
+
 def launch_list(lins, merge):
     """The step's launches: (name, N, K, abits).  merge: gate and up, which read the same input,
     run as one linear over their concatenated weights (one image [2N, K]; output [gate | up])."""
@@ -299,7 +304,12 @@ def fp16_compare(shapes, M, abits, dev, reps=20, int8=False):
         t16 = time_graph(g16, 5, s) / (5 * reps)
         t6 = time_graph(g6, 5, s) / (5 * reps)
         row = {"N": N, "K": K, "M": M, "fp16_us": round(t16 * 1e6, 2), "w6_us": round(t6 * 1e6, 2),
-               "speedup": round(t16 / t6, 3)}
+               "speedup": round(t16 / t6, 3),
+               # what the vendor GEMV achieves (a weak one inflates the speedup) and the W6 kernel's own
+               # roofline fraction -- the figure the north-star verdict rests on
+               "fp16_TBps": round(fp16_bytes(M, N, K) / t16 / 1e12, 3),
+               "w6_hbm_frac": round(alg_bytes(M, N, K, abits, ops.act_scratch_bytes(M, N, K) == 0) / t6 / 1e9
+                                    / HBM_PEAK_GBS, 4)}
         del g16, g6, w16, wq
         torch.cuda.synchronize()
         if int8:
@@ -324,7 +334,8 @@ def reference_sweep(dev, Ms=(1, 2, 4, 8), reps=10, budget=512 * 2**20):
     Averages per M in README.md:189's form: the arithmetic mean of the per-shape speedups."""
     g = torch.Generator(device=dev).manual_seed(11)
     s = torch.cuda.Stream(dev)
-    rows, by_m = [], {m: {"vs_int8": [], "vs_fp16": [], "linear_vs_int8": []} for m in Ms}
+    rows, by_m = [], {m: {"vs_int8": [], "vs_fp16": [], "linear_vs_int8": [], "fp16_TBps": [], "w6_frac": []}
+                      for m in Ms}
     for (model, N, K, ab) in REFERENCE_SWEEP:
         c16 = max(2, -(-budget // (2 * N * K)))
         c6 = max(2, -(-budget // (N * K * 3 // 4)))
@@ -353,8 +364,12 @@ def reference_sweep(dev, Ms=(1, 2, 4, 8), reps=10, budget=512 * 2**20):
                 del gr
             row = {"model": model, "M": M, "N": N, "K": K, "abits": ab, "w6_gemm_us": round(t["gemm"] * 1e6, 2),
                    "w6_linear_us": round(t["lin"] * 1e6, 2), "fp16_us": round(t["fp16"] * 1e6, 2),
-                   "speedup_vs_fp16": round(t["fp16"] / t["gemm"], 3)}
+                   "speedup_vs_fp16": round(t["fp16"] / t["gemm"], 3),
+                   "fp16_TBps": round(fp16_bytes(M, N, K) / t["fp16"] / 1e12, 3),
+                   "w6_gemm_hbm_frac": round(alg_bytes(M, N, K, ab, False) / t["gemm"] / 1e9 / HBM_PEAK_GBS, 4)}
             by_m[M]["vs_fp16"].append(t["fp16"] / t["gemm"])
+            by_m[M]["fp16_TBps"].append(row["fp16_TBps"])
+            by_m[M]["w6_frac"].append(row["w6_gemm_hbm_frac"])
             if ti is not None:
                 row.update(int8_us=round(ti * 1e6, 2), int8_M=mi, speedup_vs_int8=round(ti / t["gemm"], 3),
                            linear_speedup_vs_int8=round(ti / t["lin"], 3))
@@ -374,6 +389,8 @@ def reference_sweep(dev, Ms=(1, 2, 4, 8), reps=10, budget=512 * 2**20):
             "avg_speedup_vs_int8_by_M": {str(m): mean(v["vs_int8"]) for m, v in by_m.items()},
             "avg_linear_speedup_vs_int8_by_M": {str(m): mean(v["linear_vs_int8"]) for m, v in by_m.items()},
             "avg_speedup_vs_fp16_by_M": {str(m): mean(v["vs_fp16"]) for m, v in by_m.items()},
+            "avg_fp16_TBps_by_M": {str(m): mean(v["fp16_TBps"]) for m, v in by_m.items()},
+            "avg_w6_gemm_hbm_frac_by_M": {str(m): mean(v["w6_frac"]) for m, v in by_m.items()},
             "shapes": rows}
 
 
@@ -488,6 +505,82 @@ def cpu_baseline(budget_s=15.0, lins=None, M=1):
                                                         layers=req_layers, seconds=round(req_dt, 2),
                                                         note="the reference eval flow (flexqllm.py:106-108)"),
                 })
+
+
+# ---- the driver's line: the driver keeps a ~8 KB tail of stdout, so the final line must stay short
+# (round 4's 28 KB line was unparseable).  The full result goes to a detail file; the line keeps the
+# headline, the rooflines, the CPU baseline and per-section summaries.
+LINE_MAX = 6000
+ESSENTIAL = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+# optional sections, dropped from the line in this order while it is too long (all stay in the detail file)
+DROP_ORDER = ("vs_reference_sweep", "decoder_layers_e2e", "tp_llama2_7b_peer_gather", "tp_peer_gather",
+              "c4_llama2_70b_tp_peer_gather", "replicas", "vs_rocblas_fp16", "tp_llama2_7b", "c4_llama2_70b_tp",
+              "c4_llama2_70b_1gpu", "c3_llama2_7b_m16", "c5_llama3_8b_prefill", "tp", "decode_chain")
+_TEXT_KEYS = {"what", "method", "traffic_vs", "note", "cores_reason", "hardware"}
+_ROW = ("N", "K", "M", "fp16_us", "w6_us", "speedup", "fp16_TBps", "w6_hbm_frac")
+
+
+def _slim(v):
+    """Drop explanatory text (it is in the detail file and DESIGN.md) and round floats."""
+    if isinstance(v, dict):
+        return {k: _slim(x) for k, x in v.items() if k not in _TEXT_KEYS}
+    if isinstance(v, list):
+        return [_slim(x) for x in v]
+    if isinstance(v, float):
+        return round(v, 4)
+    return v
+
+
+def compact_line(res, detail=None, limit=LINE_MAX):
+    """The one JSON object bench.py prints last: every ESSENTIAL key, then the optional sections with
+    their per-shape rows folded into summaries (vs_reference_sweep: the per-M averages only;
+    vs_rocblas_fp16: one short row per shape), dropping whole sections in DROP_ORDER while the line is
+    longer than `limit` characters."""
+    out = {}
+    for k, v in res.items():
+        if k == "vs_reference_sweep" and isinstance(v, dict) and "shapes" in v:
+            v = {kk: vv for kk, vv in v.items() if kk != "shapes"}
+            v["shapes_count"] = len(res[k]["shapes"])
+        elif k == "vs_rocblas_fp16" and isinstance(v, dict):
+            v = dict(v)
+            for kk in ("config_shapes", "llama2_70b_m1"):
+                if isinstance(v.get(kk), list):
+                    v[kk] = [[r.get(f) for f in _ROW] for r in v[kk]]
+            v["row_fields"] = list(_ROW)
+        elif k == "cpu_baseline" and isinstance(v, dict):
+            req = v.get("variants", {}).get("requant_weights_per_forward", {})
+            v = {kk: vv for kk, vv in v.items() if kk != "variants"}
+            if req:
+                v["requant_weights_per_forward_value"] = req.get("value")
+        out[k] = _slim(v)
+    if detail:
+        out["detail_file"] = detail
+    for k in DROP_ORDER:
+        if len(json.dumps(out)) <= limit:
+            break
+        if k in out:
+            out[k] = "in detail_file"
+    if len(json.dumps(out)) > limit:  # last resort: the essentials alone
+        out = {k: out[k] for k in ESSENTIAL if k in out}
+        if detail:
+            out["detail_file"] = detail
+    return out
+
+
+def write_detail(res, path):
+    """The full result as JSON (every row of every comparison); returns the path written, or None."""
+    if not path:
+        return None
+    try:
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(res, f)
+        return os.path.relpath(path, ROOT) if os.path.abspath(path).startswith(ROOT) else path
+    except OSError as e:
+        print(f"[bench] could not write {path}: {e}", file=sys.stderr)
+        return None
 
 
 def visible_gpus():
@@ -775,8 +868,17 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
         if tp > 1 and not ctx.staged:
             dist.all_reduce(t)
 
-    def step_w6(h, reduce=True):  # each layer's last residual add fused into the next one's norm (FT)
-        run_layers(w6, h, reduce=reduce)
+    def step_w6(h):  # each layer's last residual add fused into the next one's norm (FT)
+        run_layers(w6, h)
+
+    def step_w6_noreduce(h):  # tp > 1, timing only: the same launches on the same buffers with the two
+        # all-reduces per layer left out (every rank's partial sums feed its next norm: not a model output;
+        # run_layers refuses reduce=False at tp > 1 for exactly that reason, so this bypasses it on purpose)
+        pending, cur, spare = None, h, torch.empty_like(h)
+        for L in w6:
+            pending, cur, spare = L.step(cur, pending, spare, reduce=False)
+        if pending is not None:
+            torch.add(cur, pending, out=h)
 
     def step_w6_chain(h):  # the same layers as decode chains (one launch per layer at M = 1; one rank)
         run_layers_chained(w6, h)
@@ -803,7 +905,7 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
         hs["w6_chain"] = h0.clone()
         fns["w6_chain"] = lambda: step_w6_chain(hs["w6_chain"])
     if tp > 1:
-        fns["w6_noreduce"] = lambda: step_w6(hs["w6_noreduce"], reduce=False)
+        fns["w6_noreduce"] = lambda: step_w6_noreduce(hs["w6_noreduce"])
     finals = {}
     for name, fn in fns.items():
         replay = ctx.prepare(fn, not ctx.a.no_graph and not ctx.staged)
@@ -901,6 +1003,9 @@ def main():
     ap.add_argument("--no-chain", action="store_true",
                     help="N = 1 decode: time only one launch per linear (default: also the decode chains, "
                          "fq_linear_chain_w6ax, taken for `value` when bit-identical and faster)")
+    ap.add_argument("--detail-out", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="file for the full result (every comparison row); the printed line is its summary "
+                         "(<= %d chars, what the driver parses); '' = none" % LINE_MAX)
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo with host-staged gathers, no graph")
     a = ap.parse_args()
@@ -1226,7 +1331,7 @@ def main():
     if rank == 0 and world == 1 and a.cpu_budget > 0:
         res["cpu_baseline"] = cpu_baseline(a.cpu_budget, lins, M)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(compact_line(res, write_detail(res, a.detail_out))), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -19,7 +19,9 @@ if os.environ.get("FLEXQ_AMD_LIB"):
     LIB_PATH = os.path.abspath(os.environ["FLEXQ_AMD_LIB"])
 
 FQ_OK = 0
-_STATUS = {1: "FQ_ERR_NULL", 2: "FQ_ERR_SHAPE", 3: "FQ_ERR_BITS", 4: "FQ_ERR_WORKSPACE", 5: "FQ_ERR_HIP"}
+FQ_ERR_TIMEOUT = 6
+_STATUS = {1: "FQ_ERR_NULL", 2: "FQ_ERR_SHAPE", 3: "FQ_ERR_BITS", 4: "FQ_ERR_WORKSPACE", 5: "FQ_ERR_HIP",
+           6: "FQ_ERR_TIMEOUT"}
 
 
 class FlexQExtensionError(RuntimeError):
@@ -32,6 +34,11 @@ class FlexQError(RuntimeError):
     def __init__(self, fn, status):
         super().__init__(f"{fn} failed: {_STATUS.get(status, status)} ({status})")
         self.status = status
+
+
+class ChainTimeoutError(FlexQError):
+    """FQ_ERR_TIMEOUT: a decode chain's in-kernel wait timed out on this chain workspace earlier; that
+    launch's results and every later one's are undefined until ops.chain_reset()."""
 
 
 P = ctypes.c_void_p
@@ -57,6 +64,9 @@ _SIGS = {
     "fq_chain_workspace_init": ([P, SZ, P], I),
     "fq_chain_error_offset": ([], SZ),
     "fq_chain_workspace_bytes": ([P, I, I], SZ),
+    "fq_chain_bind_status": ([P, P, P], I),
+    "fq_chain_status": ([P], I),
+    "fq_chain_reset": ([P, SZ, P], I),
     "fq_ref_bit_packing": ([P, P, I, I, I, P], I),
     "fq_ref_quantize_bit_packing": ([P, P, P, I, I, I, P], I),
     "fq_import_ref_w": ([P, P, I, I, P, P], I),
@@ -127,6 +137,8 @@ def load():
 def call(name, *args):
     """Invoke an fq_status-returning entry point and raise on failure."""
     rc = getattr(load(), name)(*args)
+    if rc == FQ_ERR_TIMEOUT:
+        raise ChainTimeoutError(name, rc)
     if rc != FQ_OK:
         raise FlexQError(name, rc)
 

@@ -15,7 +15,7 @@ fq_status fq_rmsnorm_quantize_to(const uint16_t *input, const uint16_t *residual
                                  const uint16_t *gamma, float eps, int M, int K, int abits, int8_t *xq, uint16_t *xs,
                                  uint16_t *normed_out, fq_stream_t stream);
 
-extern "C" const char *fq_version(void) { return "flexq_amd 0.3.0 (gfx950, int8-MFMA W6Ax)"; }
+extern "C" const char *fq_version(void) { return "flexq_amd 0.4.0 (gfx950, int8-MFMA W6Ax)"; }
 extern "C" int fq_abi_version(void) { return FQ_ABI_VERSION; }
 
 extern "C" const char *fq_status_string(fq_status s) {
@@ -26,6 +26,7 @@ extern "C" const char *fq_status_string(fq_status s) {
         case FQ_ERR_BITS: return "unsupported bit width (W6 with A6 or A8)";
         case FQ_ERR_WORKSPACE: return "workspace missing or too small";
         case FQ_ERR_HIP: return "HIP launch failed";
+        case FQ_ERR_TIMEOUT: return "a decode chain wait timed out on this chain workspace (fq_chain_reset)";
         default: return "unknown status";
     }
 }

@@ -30,12 +30,14 @@ struct Scratch {
 // Library-owned device memory of the instances: never freed while the process runs (a captured
 // graph bakes these addresses in), superseded buffers retired instead.
 std::mutex g_mu;
-// an imported weight image, the stream its import was enqueued on and an event recorded behind the
-// import (null when the import was captured into a graph)
+// an imported weight image, the stream its import was enqueued on, an event recorded behind an eager
+// import (null once it has completed), and whether the import was captured into a graph (it then runs
+// only when the graph replays: no other stream may use the image)
 struct Image {
     void *img;
     hipStream_t owner;
     hipEvent_t ready;
+    bool captured;
 };
 std::map<WeightKey, Image> g_images;
 std::map<hipStream_t, Scratch> g_scratch;
@@ -78,10 +80,23 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
     if (it != g_images.end()) {
         // another stream's first use must not overtake the import enqueued on the owner's stream
         Image &im = it->second;
+        if (s != im.owner && im.captured) {  // filled by a graph replay only: nothing orders another stream
+            report(FQ_ERR_HIP, "FQBMMA exec: weight image imported inside a graph capture, used from another stream "
+                               "(run the first exec eagerly, or only on the capturing stream)");
+            return nullptr;
+        }
         if (im.ready && s != im.owner) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
             if (hipEventQuery(im.ready) == hipSuccess) {
                 (void)hipEventDestroy(im.ready);
                 im.ready = nullptr;  // the import has completed: no stream needs to wait any more
+            } else if (capturing) {
+                // an event recorded outside this capture cannot order a captured node: refuse rather than
+                // record a graph without the dependency
+                report(FQ_ERR_HIP, "FQBMMA exec: captured use of a weight image whose eager import is still in "
+                                   "flight on another stream (synchronise before capturing)");
+                return nullptr;
             } else if (hipStreamWaitEvent(s, im.ready, 0) != hipSuccess) {
                 report(FQ_ERR_HIP, "FQBMMA exec: ordering against the weight import");
                 return nullptr;
@@ -103,12 +118,13 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
     }
     hipEvent_t ready = nullptr;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
-        hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess && hipEventRecord(ready, s) != hipSuccess) {
+    const bool captured = !(hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone);
+    if (!captured && hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess &&
+        hipEventRecord(ready, s) != hipSuccess) {
         (void)hipEventDestroy(ready);
         ready = nullptr;
     }
-    g_images[key] = Image{img, s, ready};
+    g_images[key] = Image{img, s, ready, captured};
     g_device_bytes += bytes;
     return img;
 }

@@ -15,6 +15,8 @@
 // weight layout stores exactly these B operands (16-column tiles, fq_quant.hip).
 #include "fq_lds.h"
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 #include <type_traits>
 
 // =============================================================================================
@@ -220,7 +222,17 @@ constexpr int FQ_CHAIN_MAX = 8;
 constexpr size_t FQ_CHAIN_SYNC_BYTES = 4096;       // chain workspace: sync words, then the hand-offs
 constexpr int FQ_CHAIN_EPOCH = 8, FQ_CHAIN_ERR = 9, FQ_CHAIN_DONE = 10;  // sync words, 128 B apart;
                                                                            // 0..7: the start counter
+constexpr int FQ_CHAIN_HOST = 11;  // 8 bytes: device address of the bound host status word (or 0)
 __device__ __forceinline__ uint32_t chain_tag(uint32_t epoch) { return epoch + 1u; }
+// A wait timed out: the sticky device error word (later waits on this workspace return at once) and,
+// when the caller bound one (fq_chain_bind_status), the host status word -- a system-scope vector store
+// into pinned host memory, read by the host entry point before its next launch (FQ_ERR_TIMEOUT).
+__device__ __forceinline__ void chain_fail(uint32_t *__restrict__ sync) {
+    __hip_atomic_store(sync + 32 * FQ_CHAIN_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t h = __hip_atomic_load(reinterpret_cast<uint64_t *>(sync + 32 * FQ_CHAIN_HOST), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if (h) __hip_atomic_store(reinterpret_cast<uint32_t *>(h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // The epoch is loaded as the launch starts and first needed a linear later: every use goes through
 // this (volatile: not hoisted to the load), so no wave waits for it before its first DMA.
 __device__ __forceinline__ uint32_t chain_late(uint32_t v) {
@@ -255,7 +267,7 @@ __device__ __forceinline__ void chain_epoch_update(uint32_t *__restrict__ sync, 
         if (!ok) ok = __hip_atomic_load(sync + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
     }
     if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
-        if (lane == 0) __hip_atomic_store(sync + 32 * FQ_CHAIN_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) chain_fail(sync);
     } else if (lane < 8) {
         __hip_atomic_store(sync + 32 * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane == 0) __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -760,7 +772,7 @@ __device__ __forceinline__ void decode_body(
                     __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
                     if (spin == (1 << 20) - 1) {
                         failed = true;
-                        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (lane == 0) chain_fail(pro.chain);
                     }
                 }
             }
@@ -814,7 +826,7 @@ __device__ __forceinline__ void decode_body(
                 __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
                 if (spin == (1 << 20) - 1) {
                     failed = true;
-                    if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) chain_fail(pro.chain);
                 }
             }
             FQ_CSTAMP(6);
@@ -1301,13 +1313,15 @@ struct ChainTail {
     int n;                     // >= 2
     uint32_t pad[PAD];         // (producer: the argument block is >= 1 KiB, the copy reads 1 KiB)
 };
-typedef ChainTail<ChainLinkPlain, 1> ChainTailPlain;
+typedef ChainTail<ChainLinkPlain, 13> ChainTailPlain;
 typedef ChainTail<ChainLinkP, 56> ChainTailP;
 constexpr int FQ_CHAIN_TAIL_OFF = 56;  // the tail's byte offset in the arguments
+// each copy reads exactly the explicit arguments (never past them into hidden arguments): the pads
+// make the argument block at least as long as the copy
 static_assert(sizeof(ChainLinkP) == 104 && FQ_CHAIN_TAIL_OFF + sizeof(ChainTailP) >= 1024 &&
               FQ_CHAIN_TAIL_OFF + offsetof(ChainTailP, pad) <= 1024, "the producer copy is 64 lanes x 16 bytes");
-static_assert(sizeof(ChainLinkPlain) == 56 && FQ_CHAIN_TAIL_OFF + offsetof(ChainTailPlain, pad) <= 512,
-              "the plain copy is 64 lanes x 8 bytes");
+static_assert(sizeof(ChainLinkPlain) == 56 && FQ_CHAIN_TAIL_OFF + sizeof(ChainTailPlain) >= 512 &&
+              FQ_CHAIN_TAIL_OFF + offsetof(ChainTailPlain, pad) <= 512, "the plain copy is 64 lanes x 8 bytes");
 template <int MT, bool CHP>
 __device__ __forceinline__ void chain_link(uint32_t *sync, int l, const ChainLinkP &L, uint32_t epoch, DecodePro pro) {
     const int N = L.w0 & 0x1fffff, abits = (L.w0 >> 21) & 15, xwin = L.w0 >> 25;
@@ -2617,6 +2631,75 @@ extern "C" fq_status fq_chain_workspace_init(void *chain_ws, size_t bytes, fq_st
     return hipMemsetAsync(chain_ws, 0, bytes, (hipStream_t)stream) == hipSuccess ? FQ_OK : FQ_ERR_HIP;
 }
 
+// ---- host-visible chain status: chain workspace -> the caller's pinned host word (host side), and the
+// word's device address in the workspace's sync area (device side, read by chain_fail)
+static std::mutex g_chain_mu;
+static std::unordered_map<const void *, volatile uint32_t *> g_chain_status;
+
+__global__ void fq_chain_bind_kernel(uint32_t *__restrict__ sync, uint64_t host_dev) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(sync + 32 * FQ_CHAIN_HOST), host_dev, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+static fq_status chain_bind(void *chain_ws, uint32_t *host_status, hipStream_t s) {
+    void *dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, host_status, 0) != hipSuccess || !dev) {
+        (void)hipGetLastError();  // (not device-mapped memory: clear the sticky error)
+        return FQ_ERR_NULL;
+    }
+    hipLaunchKernelGGL(fq_chain_bind_kernel, dim3(1), dim3(64), 0, s, (uint32_t *)chain_ws, (uint64_t)(uintptr_t)dev);
+    FQ_LAUNCH_CHECK();
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    g_chain_status[chain_ws] = host_status;
+    return FQ_OK;
+}
+
+extern "C" fq_status fq_chain_bind_status(void *chain_ws, uint32_t *host_status, fq_stream_t stream) {
+    if (!chain_ws || !host_status) return FQ_ERR_NULL;
+    if ((uintptr_t)chain_ws & 255) return FQ_ERR_WORKSPACE;
+    return chain_bind(chain_ws, host_status, (hipStream_t)stream);
+}
+
+extern "C" fq_status fq_chain_status(const void *chain_ws) {
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    const auto it = g_chain_status.find(chain_ws);
+    return it != g_chain_status.end() && *it->second != 0u ? FQ_ERR_TIMEOUT : FQ_OK;
+}
+
+extern "C" fq_status fq_chain_reset(void *chain_ws, size_t bytes, fq_stream_t stream) {
+    if (!chain_ws) return FQ_ERR_NULL;
+    const fq_status st = fq_chain_workspace_init(chain_ws, bytes, stream);
+    if (st != FQ_OK) return st;
+    uint32_t *h = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_chain_mu);
+        const auto it = g_chain_status.find(chain_ws);
+        if (it != g_chain_status.end()) h = const_cast<uint32_t *>(it->second);
+    }
+    if (!h) return FQ_OK;
+    *(volatile uint32_t *)h = 0u;  // (no launch on chain_ws is in flight: the caller synchronised)
+    return chain_bind(chain_ws, h, (hipStream_t)stream);
+}
+
+// Every workgroup of a chain launch waits on others of the same launch: the kernel must hold one
+// workgroup per CU at the run's LDS size (the grid is the CU count).  Cached per (kernel, LDS bytes).
+template <bool CHP>
+static bool chain_coresident(size_t lds) {
+    static std::mutex mu;
+    static std::unordered_map<size_t, bool> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto it = cache.find(lds);
+    if (it != cache.end()) return it->second;
+    int nb = 0;
+    const bool ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &nb, reinterpret_cast<const void *>(fq_gemm_decode_chain_kernel<4, CHP>),
+                        decode_waves(4) * 64, lds) == hipSuccess && nb >= 1;
+    if (!ok) (void)hipGetLastError();
+    cache[lds] = ok;
+    return ok;
+}
+
 // one link as its own entry point (the chain's fallback; the same bits)
 static fq_status chain_link_alone(const fq_chain_link &L, int M, int8_t *xq_buf, uint16_t *xs_buf, void *workspace,
                                   size_t workspace_bytes, fq_stream_t stream) {
@@ -2643,6 +2726,7 @@ extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int
         if (L.pro < 0 || L.pro > 2) return FQ_ERR_SHAPE;
     }
     const hipStream_t s = (hipStream_t)stream;
+    if (chain_ws && fq_chain_status(chain_ws) != FQ_OK) return FQ_ERR_TIMEOUT;  // (until fq_chain_reset)
     const bool ws_ok = chain_ws && chain_ws_bytes >= FQ_CHAIN_SYNC_BYTES && ((uintptr_t)chain_ws & 255) == 0;
     char *hand = (char *)chain_ws + FQ_CHAIN_SYNC_BYTES;  // the hand-off granules of a run
     const size_t hand_bytes = ws_ok ? (chain_ws_bytes - FQ_CHAIN_SYNC_BYTES) / 16 * 16 : 0;
@@ -2760,6 +2844,14 @@ extern "C" fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int
         }
         bool prod = false;
         for (int i = 0; i < r; i++) prod = prod || links[l + i].pro != 0;
+        if (!(prod ? chain_coresident<true>(lds) : chain_coresident<false>(lds))) {
+            for (int i = 0; i < r; i++) {  // not one workgroup per CU: the links as their entry points
+                const fq_status st = chain_link_alone(links[l + i], M, xq_buf, xs_buf, workspace, workspace_bytes, stream);
+                if (st != FQ_OK) return st;
+            }
+            l += r;
+            continue;
+        }
         if (prod) {
             ChainTailP t{};
             for (int i = 1; i < r; i++) t.l[i - 1] = cl[i];

@@ -178,7 +178,7 @@ class FlexQDecoderLayer:
         return h
 
 
-def run_layers_chained(layers, h):
+def run_layers_chained(layers, h, check=False):
     """run_layers on one rank as decode chains (ops.linear_chain_w6ax), the same bits: the first
     layer's RMSNorm + qkv alone, then per layer one chain o_i -> RMSNorm + gate_up_i -> SiLU * up +
     down_i -> RMSNorm + qkv_i+1 (the last layer's without the qkv): the linears between two attention
@@ -186,11 +186,22 @@ def run_layers_chained(layers, h):
     otherwise.  The attention core (attn_fn) must return a view of its input or a tensor computed
     before the chain (as the bench's stand-in ctx = v does): a chain cannot run a kernel between its
     links.  The residual rotates through three buffers (h and two scratch), since a chain reads one and
-    writes two.  Returns h."""
+    writes two.  Returns h.
+    Failure: a chain wait that timed out (e.g. other kernels holding CUs the chain needs, include/flexq_hip.h)
+    leaves the stream's chain workspace in the timed-out state, and the next call raises
+    _lib.ChainTimeoutError before launching anything (ops.chain_reset clears it).  check=True also
+    synchronises after the step and raises if THIS step timed out (its h is then undefined)."""
     if dist.is_initialized() and any(L.o.row_parallel and dist.get_world_size(L.o.group) > 1 for L in layers):
         raise ValueError("run_layers_chained is single-rank (tensor parallelism needs the all-reduces between links)")
     if not layers:
         return h
+    if check:
+        out = run_layers_chained(layers, h)
+        torch.cuda.current_stream(h.device).synchronize()
+        if ops.chain_status(h.device):
+            from ._lib import ChainTimeoutError
+            raise ChainTimeoutError("run_layers_chained", 6)
+        return out
     M, H = h.shape
     dev = h.device
     res = [h, torch.empty_like(h), torch.empty_like(h)]

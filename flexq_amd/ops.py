@@ -79,11 +79,13 @@ def workspace(device, nbytes, stream_handle):
 
 
 _CWS = {}  # (device, stream) -> chain workspace (fq_chain_workspace_init; written by chain launches only)
+_CWS_STATUS = {}  # id(chain workspace) -> its pinned host status word (fq_chain_bind_status), kept for the process
 
 
 def chain_workspace(device, nbytes, stream_handle):
     """Per-(device, stream) chain workspace of fq_linear_chain_w6ax: zeroed once, then written by chain
-    launches only; grown like workspace() (a superseded one a capture has seen is kept)."""
+    launches only; grown like workspace() (a superseded one a capture has seen is kept).  Each one has a
+    pinned host status word bound to it (a timed-out in-kernel wait sets it; chain_status reads it)."""
     key = (device, stream_handle)
     buf = _CWS.get(key)
     if buf is None or buf.numel() < nbytes:
@@ -94,6 +96,9 @@ def chain_workspace(device, nbytes, stream_handle):
             _WS_RETIRED.append(buf)
         buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
         _lib.call("fq_chain_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
+        host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        _lib.call("fq_chain_bind_status", _ptr(buf), ctypes.c_void_p(host.data_ptr()), ctypes.c_void_p(stream_handle))
+        _CWS_STATUS[id(buf)] = host
         _CWS[key] = buf
     if torch.cuda.is_current_stream_capturing():
         _WS_CAPTURED.add(id(buf))
@@ -314,7 +319,9 @@ def linear_chain_w6ax(links):
     and chain_silu(...) are rmsnorm_linear_w6ax / silu_linear_w6ax.  An input may be a view of the previous
     link's out, and an RMSNorm link's residual an earlier RMSNorm link's residual_out (the chain's
     hand-offs).  Runs that can chain (M <= 4; RMSNorm at M = 1, K = 4096) are one
-    persistent launch each.  Returns the list of outputs."""
+    persistent launch each.  Returns the list of outputs.  Raises _lib.ChainTimeoutError once an in-kernel
+    wait on this stream's chain workspace has timed out (that launch's results are undefined), until
+    chain_reset()."""
     _need(len(links) > 0, "empty chain")
     M, dev, scratch, Kmax = None, None, 0, 0
     arr = (_ChainLink * len(links))()
@@ -399,12 +406,35 @@ def chain_workspace_buffer(device=None, stream=None):
 
 def chain_error(device=None, stream=None):
     """The decode chain's sticky error word in the stream's chain workspace (0: every in-kernel wait
-    ended in time; 1: one timed out and the results since are undefined)."""
+    ended in time; 1: one timed out and the results since are undefined).  Reads device memory (a
+    synchronising copy); chain_status() reads the host-visible copy instead."""
     buf = chain_workspace_buffer(device, stream)
     if buf is None:
         return 0
     off = int(_lib.load().fq_chain_error_offset())
     return int(buf[off:off + 4].view(torch.int32).item())
+
+
+def chain_status(device=None, stream=None):
+    """True while the stream's chain workspace is in the timed-out state (fq_chain_status: the pinned host
+    word the kernel sets; no synchronisation, so it shows once the launch that timed out has finished).
+    linear_chain_w6ax then raises ChainTimeoutError until chain_reset()."""
+    buf = chain_workspace_buffer(device, stream)
+    return buf is not None and int(_lib.load().fq_chain_status(_ptr(buf))) != _lib.FQ_OK
+
+
+def chain_reset(device=None, stream=None):
+    """Clear a timed-out chain workspace (fq_chain_reset): re-zeroed on the stream, its host word cleared.
+    Synchronises the stream first (no chain launch may be in flight)."""
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    buf = chain_workspace_buffer(dev, s)
+    if buf is None:
+        return
+    s.synchronize()
+    _lib.call("fq_chain_reset", _ptr(buf), ctypes.c_size_t(buf.numel()), ctypes.c_void_p(s.cuda_stream))
 
 
 def act_scratch_bytes(M, N, K):

@@ -49,7 +49,7 @@ typedef struct ihipStream_t *fq_stream_t; /* == hipStream_t */
  * fq_bmma_init_image) and fq_bmma_state carries w_format / prepared; split-K prefill without its
  * workspace returns FQ_ERR_WORKSPACE.  A caller built against another version should compare
  * FQ_ABI_VERSION with fq_abi_version() at start-up. */
-#define FQ_ABI_VERSION 3
+#define FQ_ABI_VERSION 4   /* 4: FQ_ERR_TIMEOUT and the host-visible chain status (fq_chain_bind_status) */
 int fq_abi_version(void);
 
 typedef int fq_status;
@@ -59,6 +59,9 @@ typedef int fq_status;
 #define FQ_ERR_BITS 3      /* unsupported bit width */
 #define FQ_ERR_WORKSPACE 4 /* workspace missing or smaller than fq_gemm_workspace_bytes() */
 #define FQ_ERR_HIP 5       /* the HIP launch itself failed */
+#define FQ_ERR_TIMEOUT 6   /* a decode chain's in-kernel wait timed out earlier on this chain workspace:
+                              the results of that launch and of every later one are undefined; nothing
+                              was enqueued (fq_chain_reset clears it) */
 
 /* ---- library info ------------------------------------------------------------------------ */
 const char *fq_version(void);
@@ -141,7 +144,17 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
  * shorter one runs shorter runs or plain linears), zeroed once by fq_chain_workspace_init and then
  * written by chain launches only (one per stream; it may serve every chain of that stream).
  * A chain launch never hangs: a wait that does not end within ~1 s sets the word at byte offset
- * fq_chain_error_offset() of chain_ws (sticky; results undefined) -- the caller checks it.
+ * fq_chain_error_offset() of chain_ws (sticky; results undefined; every later wait on that workspace
+ * returns at once) and, when a host status word is bound (fq_chain_bind_status), that word too; from
+ * then on fq_linear_chain_w6ax on chain_ws returns FQ_ERR_TIMEOUT without enqueuing anything, until
+ * fq_chain_reset (the reference's convention: FQBMMAOp::initialize sets initSuccess = false and the
+ * wrapper prints and returns, flexq_bmma_op.h:103-126, flexq_gemm_wrapper.cu:93).
+ * Co-residency: every workgroup of a chain launch waits for workgroups of the same launch, so the
+ * launch needs all of its workgroups (one per CU) resident at once.  The host checks that the kernel
+ * can hold one workgroup per CU (the occupancy query; otherwise the links run as their entry points),
+ * but it cannot see CUs held by kernels of other streams or processes: a caller that overlaps other
+ * kernels with a chain (concurrent streams, several processes on one GPU) must expect a timeout there,
+ * which the status above reports.
  * No FlexQ counterpart: the reference launches one kernel per GEMM call (flexq_gemm_wrapper.cu:99-122). */
 typedef struct fq_chain_link {
     const uint16_t *x;     /* fp16 [M][K]; pro 1: the residual; pro 2: the gate (rows of stride ldh) */
@@ -162,6 +175,19 @@ fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int M, void *c
 size_t fq_chain_workspace_bytes(const fq_chain_link *links, int n, int M);
 fq_status fq_chain_workspace_init(void *chain_ws, size_t bytes, fq_stream_t stream);
 size_t fq_chain_error_offset(void);
+/* Host-visible chain status.  host_status (host): a zeroed 4-byte word of pinned, device-mapped host
+ * memory (hipHostMalloc, or torch's pinned memory), owned by the caller and kept alive with chain_ws.
+ * Binding enqueues one small kernel on `stream` that records the word's device address in chain_ws
+ * (call it after fq_chain_workspace_init).  FQ_ERR_NULL when host_status is not device-mapped. */
+fq_status fq_chain_bind_status(void *chain_ws, uint32_t *host_status, fq_stream_t stream);
+/* FQ_ERR_TIMEOUT once a wait on chain_ws timed out (the bound word, read on the host: no
+ * synchronisation, so a timeout shows once the launch that hit it has finished); FQ_OK otherwise,
+ * also for a workspace without a bound word.  A captured graph's replays do not pass through
+ * fq_linear_chain_w6ax: read this after synchronising with the replays. */
+fq_status fq_chain_status(const void *chain_ws);
+/* Clear a timed-out chain workspace: re-zero its `bytes` (stream-ordered), re-bind its host word and
+ * clear it.  No chain launch on chain_ws may be in flight (synchronise first). */
+fq_status fq_chain_reset(void *chain_ws, size_t bytes, fq_stream_t stream);
 
 /* ---- prefill with resident unpacked weights ------------------------------------------------------
  * At M >= 2048 fq_gemm_w6ax unpacks the weight image into int8 MFMA operands in its workspace on

@@ -57,6 +57,55 @@ def test_optional_section_failure_is_agreed_across_ranks():
     assert "another rank" in res[0]["first"]["error"] and "out of memory" in res[1]["first"]["error"]
 
 
+def _r04_result():
+    """Round 4's full N = 1 result (28,196 characters as one line: the driver could not parse it)."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "r04_bench_final.json")) as f:
+        return json.loads(f.readline())
+
+
+def test_driver_line_fits_and_keeps_the_headline():
+    """The printed line stays under the driver's limit on a full N = 1 result, keeps every essential key
+    (value, roofline, cpu_baseline, ...) and the per-M averages of the reference sweep, and folds the
+    per-shape rows away (they are in the detail file)."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    res = _r04_result()
+    assert len(json.dumps(res)) > 20000  # the representative input really is the oversized one
+    line = bench.compact_line(res, "gpurun_out/bench_detail.json")
+    text = json.dumps(line)
+    assert len(text) < 6000, len(text)
+    for k in bench.ESSENTIAL:
+        assert k in line, k
+    assert line["value"] == res["value"] and line["ms_per_step"] == res["ms_per_step"]
+    assert line["roofline"]["frac"] == res["roofline"]["frac"] and line["roofline"]["bound"] == "hbm"
+    assert line["cpu_baseline"]["cores"] == 16 and line["cpu_baseline"]["kind"] == "port"
+    for k in ("c3_llama2_7b_m16", "c5_llama3_8b_prefill", "c4_llama2_70b_1gpu", "decode_chain"):
+        assert isinstance(line[k], dict) and "roofline" in line[k] or k == "decode_chain", k
+    sweep = line["vs_reference_sweep"]
+    assert "shapes" not in sweep and sweep["avg_speedup_vs_int8_by_M"] == res["vs_reference_sweep"]["avg_speedup_vs_int8_by_M"]
+    assert line["detail_file"] == "gpurun_out/bench_detail.json"
+
+
+def test_driver_line_drops_sections_rather_than_overflow():
+    """Even with every multi-GPU section present and oversized, the line stays under the limit: whole
+    optional sections give way (in DROP_ORDER), never the essentials."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    res = _r04_result()
+    big = {"what": "x" * 3000, "ms_per_step": 1.0, "rows": [{"a": i, "b": float(i)} for i in range(200)]}
+    for k in ("tp", "tp_llama2_7b", "tp_peer_gather", "tp_llama2_7b_peer_gather", "c4_llama2_70b_tp",
+              "c4_llama2_70b_tp_peer_gather", "replicas"):
+        res[k] = dict(big)
+    line = bench.compact_line(res, "d.json")
+    assert len(json.dumps(line)) < 6000
+    for k in bench.ESSENTIAL:
+        assert k in line, k
+    assert bench.compact_line({k: res[k] for k in bench.ESSENTIAL if k in res})["value"] == res["value"]
+
+
 def test_chain_runs_cut_at_the_attention_cores():
     """bench.chain_runs: the step's linears in order, cut before every o_proj (the attention core sits
     between qkv and o), so 32 LLaMA layers give qkv_0 | (o, gate_up, down, qkv) x 31 | o, gate_up, down."""

@@ -193,6 +193,103 @@ def test_chain_error_word_fails_fast_and_recovers(ops, dev):
     check(ops, links, dev, "after clearing the error word")
 
 
+def test_headline_step_pinned_to_the_oracle(ops, dev):
+    """The headline step itself (bench.py's LLaMA-2-7B M = 1 stack as bench.chain_runs builds it, two layers:
+    qkv_0 | o_0, gate_up_0, down_0, qkv_1 | o_1, gate_up_1, down_1) against the CPU oracle directly, link by
+    link: each link's actual input (the chain's own previous output) quantized by the
+    oracle is bit-identical to the engine's codes and scales; the oracle's int32 group accumulators over the
+    link's weight image (unpacked by the oracle) equal the debug kernel's bit for bit
+    (engine/test_bgemm_kernel.cu:113-146's check); the chain's fp16 output equals that debug launch's bit for
+    bit and lies within oracle.gemm_tolerance of the oracle's."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from common import assert_gemm_close, oracle
+    cfg = (2, 1, bench.CONFIGS["llama2-7b-m1"][2], "two LLaMA-2-7B layers")
+    stack = bench.build_stack(cfg, 0, 1, dev, merge=True, seed=77)
+    runs = bench.chain_runs(stack)
+    assert [len(r) for r in runs] == [1, 4, 3]
+    bench.run_chains(runs)
+    torch.cuda.synchronize()
+    assert ops.chain_error(dev) == 0
+    for i, (x, pk, N, abits, out) in enumerate(link for r in runs for link in r):
+        K = x.shape[1]
+        q, s = oracle.quantize_engine(x.cpu().numpy(), abits)
+        xq, xs = ops.quantize_act(x.contiguous(), abits)
+        np.testing.assert_array_equal(xq.cpu().numpy(), q, err_msg=f"link {i}: activation codes")
+        np.testing.assert_array_equal(xs.cpu().numpy().view(np.uint16), s.view(np.uint16), err_msg=f"link {i}: scales")
+        wq, ws = oracle.unpack_fq6(pk.cpu().numpy(), N, K, want_ws=True)
+        ref, acc_ref, mag = oracle.gemm(q, s, wq, ws, want_acc=True)
+        d_dbg, acc = ops.gemm_w6ax(xq, xs, pk, N, abits, return_acc=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(acc.cpu().numpy(), acc_ref, err_msg=f"link {i}: int32 group accumulators")
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), d_dbg.cpu().numpy().view(np.uint16),
+                                      err_msg=f"link {i}: chain output vs the debug launch")
+        assert_gemm_close(out.cpu().numpy(), ref, mag, f"headline link {i} ({N}x{K})")
+
+
+def test_chain_host_status_raises_until_reset(ops, dev):
+    """A set host status word (what a timed-out wait leaves) makes the next linear_chain_w6ax raise
+    ChainTimeoutError without launching; chain_reset clears the workspace and the word, and the chain
+    computes the right bits again."""
+    from flexq_amd import _lib
+    links = build(ops, dev, 1, LAYER_7B * 2, seed=13)
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    assert not ops.chain_status(dev)
+    buf = ops.chain_workspace_buffer(dev)
+    ops._CWS_STATUS[id(buf)][0] = 1  # as chain_fail's system-scope store would
+    with pytest.raises(_lib.ChainTimeoutError):
+        ops.linear_chain_w6ax(links)
+    ops.chain_reset(dev)
+    assert not ops.chain_status(dev) and ops.chain_error(dev) == 0
+    for (*_, out) in links:
+        out.fill_(float("nan"))
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    check(ops, links, dev, "after chain_reset")
+
+
+def test_chain_not_coresident_times_out_and_recovers(ops, dev):
+    """The co-residency failure: a kernel on another stream holds half of the CUs for 2.5 s
+    while a chain launches, so half of the chain's workgroups cannot start.  The resident ones' waits end
+    after ~1 s with the error word set (never a hang); the kernel itself writes the bound host word, the
+    next call raises ChainTimeoutError, and after chain_reset the chain is bit-exact again."""
+    import ctypes
+    import os
+    import time
+    from flexq_amd import _lib
+    so = os.path.join(os.path.dirname(__file__), "cpp", "libcu_blocker.so")
+    if not os.path.exists(so):
+        pytest.skip("tests/cpp/libcu_blocker.so not built (__graft_entry__.build())")
+    blk = ctypes.CDLL(so)
+    blk.fq_test_cu_blocker.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    links = build(ops, dev, 1, LAYER_7B * 2, seed=14)
+    ops.linear_chain_w6ax(links)  # the workspace exists and is bound
+    torch.cuda.synchronize()
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    sink = torch.zeros(cus, dtype=torch.int32, device=dev)
+    side = torch.cuda.Stream(dev)
+    assert blk.fq_test_cu_blocker(cus // 2, 2500, ctypes.c_void_p(sink.data_ptr()),
+                                  ctypes.c_void_p(side.cuda_stream)) == 0
+    time.sleep(0.2)  # the blocker is resident
+    t0 = time.time()
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    assert time.time() - t0 < 30.0
+    assert ops.chain_error(dev) == 1, "the chain could not have been co-resident"
+    assert ops.chain_status(dev), "the kernel did not write the bound host status word"
+    with pytest.raises(_lib.ChainTimeoutError):
+        ops.linear_chain_w6ax(links)
+    ops.chain_reset(dev)
+    for (*_, out) in links:
+        out.fill_(float("nan"))
+    ops.linear_chain_w6ax(links)
+    torch.cuda.synchronize()
+    check(ops, links, dev, "after the co-residency timeout and chain_reset")
+
+
 def _layer_links(ops, dev, g, x_attn, h, n_layers=1):
     """A LLaMA-2-7B decoder layer's linears after the attention core as chain links (M = 1):
     o -> RMSNorm(h + o) + gate_up -> SiLU(gate) * up + down -> RMSNorm(h' + down) + next qkv.

@@ -624,6 +624,9 @@ def test_prefill_resident_weights_bit_identical(ops, dev, M, N, K):
     (8192, 6144, 1024, 8192, 4096, 8),     # qkv -> o: the next input a prefix of the output (256 x 256 epilogue)
     (4096, 28672, 1024, 8192, 14336, 8),   # gate_up -> down shape: the next rows straddle the output rows
     (4096, 4096, 1024, 4096, 4096, 6),     # A6 codes
+    # ragged M (M % 256 != 0): the epilogue kernel's XSF = false form, partial last row tile
+    (2404, 4096, 1024, 2404, 4096, 8),
+    (2404, 4096, 1024, 7000, 1280, 6),     # qK != N, the next input ending mid-row of the output
     (2048, 4096, 1024, 2048, 4096, 8),     # 128 x 128 tiles (fill rule): the GEMM, then the quantizer
     (2048, 1000, 1280, 3200, 640, 8),      # N % 128 != 0: the GEMM, then the quantizer
     (32, 4096, 4096, 32, 4096, 8),         # decode sizes: the same
