@@ -759,14 +759,23 @@ __device__ __forceinline__ void decode_body(
                     if (c + 4 * u < R) v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u], 0, 16));
             } else {
                 for (int spin = 0; spin < (1 << 20); spin++) {
+                    // every granule load of the pass in flight at once, then the tag compares (a
+                    // short-circuit && between them serialises one round trip per load pair)
+                    uint4 g0[4], g1[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (c + 4 * u < R) {
+                            g0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u], 0, 16));
+                            g1[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u] + 16, 0, 16));
+                        }
+                    }
                     bool ok = true;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        if (c + 4 * u >= R) break;
-                        const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u], 0, 16));
-                        const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u] + 16, 0, 16));
-                        v[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
-                        ok = ok && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                        if (c + 4 * u < R) {
+                            v[u] = make_uint4(g0[u].x, g0[u].z, g1[u].x, g1[u].z);
+                            ok = ok & (g0[u].y == want) & (g0[u].w == want) & (g1[u].y == want) & (g1[u].w == want);
+                        }
                     }
                     if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
                     __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
@@ -798,26 +807,40 @@ __device__ __forceinline__ void decode_body(
             // tags all matched is not loaded again (the other's re-polls do not queue behind it)
             bool dx = !gr, din = !gin;
             for (int spin = 0; spin < (1 << 20); spin++) {
+                // every load of the pass in flight at once, then the tag compares (a short-circuit &&
+                // between them serialises one round trip per load pair)
+                uint4 gx0[4], gx1[4], gi0[4], gi1[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (c + 4 * u < R) {
+                        const uint32_t el = chn_el(c, u);
+                        if (!gr) {
+                            if (spin == 0)
+                                v[u] = c == 0 ? xv0[u] : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 2, 0, 16));
+                        } else if (!dx) {
+                            gx0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4, 0, 16));
+                            gx1[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4 + 16, 0, 16));
+                        }
+                        if (hasin && !gin) {
+                            if (spin == 0) w[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 2, 0, 16));
+                        } else if (gin && !din) {
+                            gi0[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4, 0, 16));
+                            gi1[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4 + 16, 0, 16));
+                        }
+                    }
+                }
                 bool okx = true, okin = true;
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if (c + 4 * u >= R) break;
-                    const uint32_t el = chn_el(c, u);
-                    if (!gr) {
-                        if (spin == 0) v[u] = c == 0 ? xv0[u] : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 2, 0, 16));
-                    } else if (!dx) {
-                        const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4, 0, 16));
-                        const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, el * 4 + 16, 0, 16));
-                        v[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
-                        okx = okx && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
-                    }
-                    if (hasin && !gin) {
-                        if (spin == 0) w[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 2, 0, 16));
-                    } else if (gin && !din) {
-                        const uint4 g0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4, 0, 16));
-                        const uint4 g1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(inr, el * 4 + 16, 0, 16));
-                        w[u] = make_uint4(g0.x, g0.z, g1.x, g1.z);
-                        okin = okin && g0.y == want && g0.w == want && g1.y == want && g1.w == want;
+                    if (c + 4 * u < R) {
+                        if (gr && !dx) {
+                            v[u] = make_uint4(gx0[u].x, gx0[u].z, gx1[u].x, gx1[u].z);
+                            okx = okx & (gx0[u].y == want) & (gx0[u].w == want) & (gx1[u].y == want) & (gx1[u].w == want);
+                        }
+                        if (gin && !din) {
+                            w[u] = make_uint4(gi0[u].x, gi0[u].z, gi1[u].x, gi1[u].z);
+                            okin = okin & (gi0[u].y == want) & (gi0[u].w == want) & (gi1[u].y == want) & (gi1[u].w == want);
+                        }
                     }
                 }
                 dx = dx || __builtin_amdgcn_ballot_w64(!okx) == 0;  // (wave-uniform)
@@ -1270,6 +1293,29 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ln_kerne
         reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, IPW - (ir != 0), ir, 1, nullptr, pro, grid);
 }
 
+// The launch whose tag would wrap (workgroup 0 left the epoch alone): the last workgroup to arrive clears
+// every granule (all the others are done reading), the start counter and the epoch.
+__device__ __forceinline__ void chain_wrap_end(uint32_t *__restrict__ sync, uint32_t epoch, uint4 *hand,
+                                               uint32_t hand_bytes) {
+    if (chain_late(epoch) != 0xfffffffeu) return;
+    __syncthreads();
+    __shared__ uint32_t last;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's start arrival has been performed
+        last = __hip_atomic_fetch_add(sync + 32 * FQ_CHAIN_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {
+        for (uint32_t i = threadIdx.x; i < hand_bytes / 16; i += blockDim.x) hand[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x < 8) __hip_atomic_store(sync + 32 * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(sync + 32 * FQ_CHAIN_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // The decode chain's kernel: the links' packed fields (decode_pack) by value in the kernel
 // arguments (read from LDS as each linear starts); every linear runs the fused plan fq_linear_w6ax
 // would run for it (S = 1, the same grid), so the bits are the same.  Two argument layouts: a plain
@@ -1443,25 +1489,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_ke
         L.w3 = v[WO + 1].y;
         chain_link<MT, CHP>(sync, l, L, epoch, DecodePro{});
     }
-    if (chain_late(epoch) == 0xfffffffeu) {  // the tag wraps after this launch (workgroup 0 left the epoch
-        __syncthreads();                     // alone): the last workgroup to arrive clears every granule (all
-        __shared__ uint32_t last;            // the others are done reading), the start counter and the epoch
-        if (threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's start arrival has been performed
-            last = __hip_atomic_fetch_add(sync + 32 * FQ_CHAIN_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   gridDim.x - 1;
-        }
-        __syncthreads();
-        if (last) {
-            for (uint32_t i = threadIdx.x; i < t.hand_bytes / 16; i += blockDim.x) t.hand[i] = make_uint4(0, 0, 0, 0);
-            if (threadIdx.x < 8)
-                __hip_atomic_store(sync + 32 * threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (threadIdx.x == 0) {
-                __hip_atomic_store(sync + 32 * FQ_CHAIN_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(sync + 32 * FQ_CHAIN_EPOCH, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
+    chain_wrap_end(sync, epoch, t.hand, t.hand_bytes);
 }
 
 // Wait until every rank of a peer-store gather has published this generation (one workgroup; lane q

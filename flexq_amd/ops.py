@@ -96,9 +96,10 @@ def chain_workspace(device, nbytes, stream_handle):
             _WS_RETIRED.append(buf)
         buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
         _lib.call("fq_chain_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
-        host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        _lib.call("fq_chain_bind_status", _ptr(buf), ctypes.c_void_p(host.data_ptr()), ctypes.c_void_p(stream_handle))
-        _CWS_STATUS[id(buf)] = host
+        if hasattr(_lib.load(), "fq_chain_bind_status"):  # (an older A/B build may lack it)
+            host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            _lib.call("fq_chain_bind_status", _ptr(buf), ctypes.c_void_p(host.data_ptr()), ctypes.c_void_p(stream_handle))
+            _CWS_STATUS[id(buf)] = host
         _CWS[key] = buf
     if torch.cuda.is_current_stream_capturing():
         _WS_CAPTURED.add(id(buf))
