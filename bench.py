@@ -864,8 +864,8 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
         w16.append(dict(qkv=qkv_p, o=o_p, gu=gu_p, down=down_p, ga=ga, Fp=down_p.shape[1]))
     torch.cuda.synchronize()
 
-    def allreduce(t):
-        if tp > 1 and not ctx.staged:
+    def allreduce(t):  # the same all-reduces as the W6 layers' (gloo in the --share-gpu rehearsal)
+        if tp > 1:
             dist.all_reduce(t)
 
     def step_w6(h):  # each layer's last residual add fused into the next one's norm (FT)

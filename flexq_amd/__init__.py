@@ -10,4 +10,4 @@ Layers:
 """
 __version__ = "0.1.0"
 
-from ._lib import FlexQError, FlexQExtensionError  # noqa: F401
+from ._lib import ChainTimeoutError, FlexQError, FlexQExtensionError  # noqa: F401
