@@ -61,7 +61,7 @@ PY
 # 5. prefill PMC passes (one GEMM shape, the U8 big-tile kernel) and their per-dispatch averages
 echo "[profile_round] 5. prefill PMC passes (one GEMM shape, the U8 big-tile ker" ; date
 rm -rf gpurun_out/pf0 gpurun_out/pf1 gpurun_out/pf2 gpurun_out/pf3 gpurun_out/pf4 gpurun_out/pf5
-bash tools/pfprof.sh
+PF_SHAPE="${PF_SHAPE:-16384 28672 4096}" bash tools/pfprof.sh
 for i in 0 5 1 2 3 4; do python3 tools/pmc_avg.py gpurun_out/pf$i fq_gemm_prefill; done > $P/${R}_prefill_pmc.txt
 grep "TOPS" gpurun_out/pf1.log | tail -1 >> $P/${R}_prefill_pmc.txt
 python3 tools/pmc_summary.py gpurun_out/pf0/p_counter_collection.csv fq_gemm_prefill prefill-16384x4096x4096 $P/${R}_prefill_fetch_summary.json > /dev/null
