@@ -335,6 +335,9 @@ struct DecodePro {
     uint32_t cdesc_lds;     //     plain chains: 512 B, loaded as the launch starts (dvx, dvy per lane);
     uint64_t kargs;         //     producer chains: 1 KiB, loaded behind linear 0's ring from kargs
     uint32_t dvx, dvy;
+    uint32_t nxt_w, nxt_p;  //   LDS addresses of the next linear's weight pointer and packed fields (its
+                            //   ring is issued by this linear's tail), or 0: the last linear
+    bool pre;               //   this linear's ring was issued by the previous linear's tail
 };
 
 // ---- fq6 weight unpack ----------------------------------------------------------------------

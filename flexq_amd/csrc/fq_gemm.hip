@@ -377,6 +377,69 @@ __device__ __forceinline__ void dequant4(float (&c)[4], v4i acc, __half2 p01, __
     c[3] = fmaf((float)acc[3], __high2float(p23), c[3]);
 }
 
+// The decode chain's next linear, started by this linear's tail: its ring's first D weight blocks and
+// its w-scale staging -- exactly the DMAs, slots and order its own prologue would issue (decode_body,
+// V2 fused plan, S = 1: t0 = the WG, tstep = the grid) -- right after this linear's last barrier (the
+// dynamic LDS is free from there).  The next linear's input wait is a wait for every older DMA of the
+// wave (vmcnt retires in order), so issuing its ring here instead of after the descriptor read and
+// the prologue's index math moves that wait earlier.  nxt_w / nxt_p: LDS addresses of the next link's
+// weight pointer and packed fields (decode_pack).
+#ifndef FQ_CHAIN_AHEAD
+#define FQ_CHAIN_AHEAD 1
+#endif
+template <int MT>
+__device__ __forceinline__ void chain_ring_ahead(uint32_t nxt_w, uint32_t nxt_p) {
+    using C = DecodeCfg<MT, 0, 0>;
+    constexpr int NW = decode_waves(MT), D = C::D;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint2 wp, pa, pb;
+    asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %4\n\tds_read_b64 %2, %4 offset:8\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(wp), "=&v"(pa), "=&v"(pb)
+                 : "v"(nxt_w), "v"(nxt_p)
+                 : "memory");
+    const uint64_t wa = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(wp.x) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(wp.y) << 32);
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(pa.x), w1 = __builtin_amdgcn_readfirstlane(pa.y);
+    const uint32_t w2 = __builtin_amdgcn_readfirstlane(pb.x), w3 = __builtin_amdgcn_readfirstlane(pb.y);
+    const int N = w0 & 0x1fffff, xwin = w0 >> 25, K = (w1 & 0x1fff) * FQ_GROUP;
+    const int IPW = w2 & 0xffff, M = w3 & 1023, ir = (w3 >> 10) & 2047, grid = w3 >> 21;
+    const int G = K / FQ_GROUP, NT = (N + 15) / 16, lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), bid = blockIdx.x;
+    const int nit = IPW - (ir != 0) + (bid < ir ? 1 : 0);
+    const int ngmax = (G + NW - 1) / NW, ga = (wid * G) / NW, ng = ((wid + 1) * G) / NW - ga, n = ng * nit;
+    if (n <= 0) return;
+    char *ring = smem + wid * decode_wave_lds(MT, 0, 0, ngmax, ngmax * IPW, M, xwin, decode_pro_windows(0));
+    char *ws_st = ring + D * C::SLOT;
+    const uint32_t *wpk = reinterpret_cast<const uint32_t *>(wa);
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, (int)((uint32_t)NT * G * FQ_BLOCK), 0x00020000);
+    const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
+    const uint32_t wvo = lane * 16, rjump = ((uint32_t)grid * G - ng + 1) * FQ_BLOCK;
+    uint32_t roff = ((uint32_t)bid * G + ga) * FQ_BLOCK;
+    int rj = 0;
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+        char *dst = ring + i * C::SLOT;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst), 16, wvo, roff, 0, FQ_W_AUX);
+        if (lane < 32) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + 1024), 16, wvo, roff + 1024, 0, FQ_W_AUX);
+        if (i + 1 < n) {  // (a short sequence re-issues its last block)
+            if (++rj == ng) {
+                rj = 0;
+                roff += rjump;
+            } else {
+                roff += FQ_BLOCK;
+            }
+        }
+        if (i == 0) {  // the w-scales, 32 blocks (32 B = 2 lanes each) per instruction (decode_body's stage_all)
+            for (int i0 = 0; i0 < n; i0 += 32) {
+                const int b = i0 + (lane >> 1) < n ? i0 + (lane >> 1) : n - 1;
+                __builtin_amdgcn_global_load_lds(wsb + ((long)(bid + (b / ng) * grid) * G + ga + b % ng) * 16 + 8 * (lane & 1),
+                                                 LDS_PTR(ws_st + i0 * 32), 16, 0, 0);
+            }
+        }
+    }
+}
+
 // FUSE: the kernel quantizes the fp16 activations itself (fq_linear_w6ax): each wave runs the
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
@@ -712,12 +775,15 @@ __device__ __forceinline__ void decode_body(
             roff += FQ_BLOCK;
         }
     };
+    // (a chain linear after the first: the previous linear's tail issued these, chain_ring_ahead;
+    // only the issue position advances here)
+    const bool pre = CHN && FQ_CHAIN_AHEAD && pro.pre;
     if (n > 0) {
 #pragma unroll
         for (int i = 0; i < D; i++) {
-            issue(rit, rj, i);
+            if (!pre) issue(rit, rj, i);
             if (i + 1 < n) advance();  // (a short sequence re-issues its last block)
-            if (i == 0) stage_all();
+            if (i == 0 && !pre) stage_all();
         }
     }
     FQ_STAMP(1);
@@ -1175,6 +1241,7 @@ __device__ __forceinline__ void decode_body(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         FQ_CSTAMP(5);
+        if (FQ_CHAIN_AHEAD && pro.nxt_w) chain_ring_ahead<MT>(pro.nxt_w, pro.nxt_p);
         return;
     }
     // GAT is a separate instantiation: the gather's branches and publish step cost the plain
@@ -1410,6 +1477,9 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_ke
     }
     p0r.cwrite = true;
     p0r.cdesc_lds = lds_addr(cdesc);
+    // link 1's descriptor (the tail's first link; a run has >= 2 links), for linear 0's tail
+    p0r.nxt_w = lds_addr(cdesc) + FQ_CHAIN_TAIL_OFF + offsetof(LINK, w);
+    p0r.nxt_p = lds_addr(cdesc) + FQ_CHAIN_TAIL_OFF + offsetof(LINK, w0);
     // the launch's epoch (used through chain_late, a linear later)
     const uint32_t epoch = __hip_atomic_load(sync + 32 * FQ_CHAIN_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ChainLinkP L0{};
@@ -1487,7 +1557,13 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_chain_ke
         L.w1 = v[WO].y;
         L.w2 = v[WO + 1].x;
         L.w3 = v[WO + 1].y;
-        chain_link<MT, CHP>(sync, l, L, epoch, DecodePro{});
+        DecodePro pr{};
+        pr.pre = true;  // (linear l - 1's tail issued this linear's ring)
+        if (l + 1 < n) {
+            pr.nxt_w = cb + 4 * (T0 + l * LW) + offsetof(LINK, w);
+            pr.nxt_p = cb + 4 * (T0 + l * LW) + offsetof(LINK, w0);
+        }
+        chain_link<MT, CHP>(sync, l, L, epoch, pr);
     }
     chain_wrap_end(sync, epoch, t.hand, t.hand_bytes);
 }
@@ -1546,13 +1622,6 @@ constexpr int PF_BSTAGE = PF_TILES * 2 * 1024;     // unpacked B: [tile][k-step]
 constexpr int PF_VM_A = 5, PF_VM_W = 3;            // per wave and group: A + scale DMAs, weight planes
 // s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
 constexpr int vmcnt_only(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
-
-template <int OFF>
-__device__ __forceinline__ uint32_t ds_read_b32_at(uint32_t a) {
-    uint32_t v;
-    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-    return v;
-}
 
 // ABL (development ablations, FQ_DEV_ABLATION builds only): 1 = no dequant (accumulators kept
 // alive, no VALU), 2 = no MFMA (operands kept alive), 4 = no compute-side LDS reads, 8 = no
@@ -1742,11 +1811,10 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
         // Blocks j = (mi, ni) in order, the dequant of block j - 1 pinned after the MFMAs of block j
         // (as in fq_gemm_prefill_big_kernel: the accumulators' latency is covered by those MFMAs)
         v4i accq[2];
-        __half2 x2s[2];
         auto dequant = [&](const v4i acc, int mi, int ni) {
-            const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
-            const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2s[mi & 1]);  // fp16-rounded
-            const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2s[mi & 1]);  // scale product
+            // the fp16-rounded scale products w * xs (v_pk_mul_f16, xs broadcast by op_sel_hi)
+            const uint32_t q01 = pk_mul_f16_lo(wv[ni][0], xv[mi]), q23 = pk_mul_f16_lo(wv[ni][1], xv[mi]);
+            const __half2 p01 = __builtin_bit_cast(__half2, q01), p23 = __builtin_bit_cast(__half2, q23);
             float *o = out[mi][ni];
             o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
             o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
@@ -1769,11 +1837,9 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
                     if (mi == 1) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xv[1]));
                     if (mi == 2) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[2][0]), "+v"(a[2][1]), "+v"(xv[2]));
                     if (mi == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[3][0]), "+v"(a[3][1]), "+v"(xv[3]));
-                    const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);  // half2(xs, xs)
-                    x2s[mi & 1] = *reinterpret_cast<const __half2 *>(&x2u);
                 }
                 if (ABL & 2) {
-                    asm volatile("" ::"v"(a[mi][0]), "v"(a[mi][1]), "v"(b[ni][0]), "v"(b[ni][1]), "v"(x2s[mi & 1]), "v"(wv[ni]));
+                    asm volatile("" ::"v"(a[mi][0]), "v"(a[mi][1]), "v"(b[ni][0]), "v"(b[ni][1]), "v"(xv[mi]), "v"(wv[ni]));
                 } else {
                     // weights as the A operand: acc[r] = column 4 (lane >> 4) + r, row lane & 15
                     v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{0, 0, 0, 0}, 0, 0, 0);
@@ -1784,7 +1850,7 @@ __global__ __launch_bounds__(PF_WAVES * 64, 2) void fq_gemm_prefill_kernel(
             if (j > 0 && !(ABL & 2)) {
                 const int pj = j - 1;
                 if (ABL & 1)
-                    asm volatile("" ::"v"(accq[pj & 1]), "v"(x2s[(pj >> 2) & 1]), "v"(wv[pj & 3]));
+                    asm volatile("" ::"v"(accq[pj & 1]), "v"(xv[pj >> 2]), "v"(wv[pj & 3]));
                 else
                     dequant(accq[pj & 1], pj >> 2, pj & 3);
             }
@@ -1947,36 +2013,50 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     const int v4 = wid & 3;
     const int swz = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;  // (row & 7 == (lane >> 3) & 7 for all 8 pieces)
     const int srow = 64 * v4 + lane;
-    const uint16_t *xsrc = xs + (m0 + srow < M ? m0 + srow : M - 1);
     const int wt = t0 + (lane >> 1) < NT ? t0 + (lane >> 1) : NT - 1;
-    const uint16_t *wsrc = wsb + (size_t)wt * G * 16 + 8 * (lane & 1);
+    // Buffer-addressed DMA (the host keeps every operand below 4 GiB for this kernel): each piece's
+    // lane offset is fixed for the whole K loop and the group moves only the SGPR offset, so a stage
+    // costs no per-piece 64-bit address VALU (those are the DMA waves' extra VALU, which the
+    // dequant-bound loop cannot hide).  Rows past M read row M - 1 (computed, never stored).
+    const __amdgpu_buffer_rsrc_t xqr = __builtin_amdgcn_make_buffer_rsrc((void *)xq, (short)0, (int)((uint32_t)M * (uint32_t)K), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xsr = __builtin_amdgcn_make_buffer_rsrc((void *)xs, (short)0, (int)((uint32_t)M * G * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc((void *)wsb, (short)0, (int)((uint32_t)NT * G * 32), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wur = __builtin_amdgcn_make_buffer_rsrc((void *)wu, (short)0, (int)((uint32_t)NT * G * 2048), 0x00020000);
+    uint32_t aoff[8], boff[4];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int row = 64 * v4 + 8 * i + (lane >> 3);
+        aoff[i] = (uint32_t)(m0 + row < M ? m0 + row : M - 1) * (uint32_t)K + swz;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int ut = t0 + 4 * v4 + t < NT ? t0 + 4 * v4 + t : NT - 1;
+        boff[t] = (uint32_t)ut * G * 2048 + lane * 16;
+    }
+    const uint32_t xsoff = XSF ? (uint32_t)(m0 + 8 * lane) * 2 : (uint32_t)(m0 + srow < M ? m0 + srow : M - 1) * 2;
+    const uint32_t wsoff = ((uint32_t)wt * G * 16 + 8 * (lane & 1)) * 2;
     auto stage = [&](int g, int slot) {
         if (ABL & 8) return;
         if (!dmaw) return;
         char *buf = sa + slot * PB_ASTAGE;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int row = 64 * v4 + 8 * i + (lane >> 3);
-            const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M are computed, never stored
-            __builtin_amdgcn_global_load_lds(xq + (size_t)m * K + g * FQ_GROUP + swz,
-                                             LDS_PTR(buf + (64 * v4 + 8 * i) * FQ_GROUP), 16, 0, 0);
-        }
+        for (int i = 0; i < 8; i++)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xqr, LDS_PTR(buf + (64 * v4 + 8 * i) * FQ_GROUP), 16, aoff[i],
+                                                     g * FQ_GROUP, 0, 0);
         if (XSF) {
             if (wid == 5 && lane < 32)
-                __builtin_amdgcn_global_load_lds(xs + (size_t)g * M + m0 + 8 * lane, LDS_PTR(buf + PB_XS_OFF), 16, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, LDS_PTR(buf + PB_XS_OFF), 16, xsoff, g * M * 2, 0, 0);
         } else {
-            __builtin_amdgcn_global_load_lds(xsrc + (size_t)g * M, LDS_PTR(buf + PB_XS_OFF + 64 * v4 * 4), 2, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, LDS_PTR(buf + PB_XS_OFF + 64 * v4 * 4), 2, xsoff, g * M * 2, 0, 0);
         }
         if (wid == 4 && lane < 32)
-            __builtin_amdgcn_global_load_lds(wsrc + g * 16, LDS_PTR(buf + PB_WS_OFF), 16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, LDS_PTR(buf + PB_WS_OFF), 16, wsoff, g * 32, 0, 0);
         char *bdst = sbu + slot * PB_BSTAGE + 4 * v4 * 2048;
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            const int ut = t0 + 4 * v4 + t < NT ? t0 + 4 * v4 + t : NT - 1;
-            const char *src = wu + ((size_t)ut * G + g) * 2048 + lane * 16;
-#pragma unroll
-            for (int k = 0; k < 2; k++)
-                __builtin_amdgcn_global_load_lds(src + k * 1024, LDS_PTR(bdst + t * 2048 + k * 1024), 16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wur, LDS_PTR(bdst + t * 2048), 16, boff[t], g * 2048, 0, 0);
+            // (the immediate offset would move the LDS destination too: the +1024 goes in the SGPR offset)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wur, LDS_PTR(bdst + t * 2048 + 1024), 16, boff[t], g * 2048 + 1024, 0, 0);
         }
     };
 
@@ -2013,7 +2093,8 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
         v4i b[4][2];
         v2u wv[4];
         v4i a[3][2];  // row blocks mi, mi + 1 and mi + 2 in flight
-        uint32_t xv[3];
+        uint32_t xv[4];  // their x-scales; slot mi % 4 lives until the dequant of (mi, 3), one block
+                         // into row mi + 1 (after row mi + 3's reads were issued into slot (mi + 3) % 4)
         if (ABL & 4) {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -2021,10 +2102,9 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                 wv[i] = v2u{ab + i, bb};
             }
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
-                a[i][0] = a[i][1] = v4i{(int)bb, (int)ab, i, g};
-                xv[i] = ab + 3 * i;
-            }
+            for (int i = 0; i < 3; i++) a[i][0] = a[i][1] = v4i{(int)bb, (int)ab, i, g};
+#pragma unroll
+            for (int i = 0; i < 4; i++) xv[i] = ab + 3 * i;
         } else {
 #define FQ_PB_B(ni)                                                \
         b[ni][0] = ds_read_b128_at<(ni) * 2048>(bb);                \
@@ -2035,7 +2115,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
 #define FQ_PB_A(mi)                                                                  \
         a[(mi) % 3][0] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off0);          \
         a[(mi) % 3][1] = ds_read_b128_at<(mi) * 16 * FQ_GROUP>(ab + a_off1);          \
-        xv[(mi) % 3] = XSF ? ds_read_u16_at<(mi) * 32>(ab + x_off) : ds_read_b32_at<(mi) * 64>(ab + x_off);
+        xv[(mi) % 4] = XSF ? ds_read_u16_at<(mi) * 32>(ab + x_off) : ds_read_b32_at<(mi) * 64>(ab + x_off);
         FQ_PB_A(0) FQ_PB_A(1)
         // in flight: B (8) + w-scales (4) + rows 0, 1 (3 each); each row block's reads are waited
         // for with the next-but-one block's (3) and the next one's (3) still outstanding
@@ -2043,16 +2123,18 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                      : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]),
                        "+v"(b[3][0]), "+v"(b[3][1]), "+v"(wv[0]), "+v"(wv[1]), "+v"(wv[2]), "+v"(wv[3]),
                        "+v"(a[0][0]), "+v"(a[0][1]), "+v"(xv[0]));
+            // (DBG: the debug output's register pressure makes the compiler spill, and a spill or copy of
+            // a read still in flight would take the old register contents: no read stays in flight)
+            if constexpr (DBG) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[1][0]), "+v"(a[1][1]), "+v"(xv[1]));
         }
+        const uint32_t ab0 = ab + a_off0, ab1 = ab + a_off1, abx = ab + x_off;  // row block reads: immediate offsets
         // Blocks j = (mi, ni) in order, the dequant of block j - 1 after the MFMAs of block j: the
         // accumulators' MFMA latency is covered by the next block's MFMAs instead of s_nops.
         v4i accq[2];
-        __half2 x2s[2];  // the x-scale pair of row blocks mi (even / odd): the dequant of (mi, 3) runs
-                         // after row block mi + 1 has taken over the slot of xv
         auto dequant = [&](const v4i acc, int mi, int ni) {
-            const uint32_t w01 = wv[ni][0], w23 = wv[ni][1];
-            const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2s[mi & 1]);  // fp16-rounded
-            const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2s[mi & 1]);  // scale product
+            // the fp16-rounded scale products w * xs (v_pk_mul_f16, xs broadcast by op_sel_hi)
+            const uint32_t q01 = pk_mul_f16_lo(wv[ni][0], xv[mi % 4]), q23 = pk_mul_f16_lo(wv[ni][1], xv[mi % 4]);
+            const __half2 p01 = __builtin_bit_cast(__half2, q01), p23 = __builtin_bit_cast(__half2, q23);
             float *o = out[mi][ni];
             o[0] = fmaf((float)acc[0], __low2float(p01), o[0]);
             o[1] = fmaf((float)acc[1], __high2float(p01), o[1]);
@@ -2073,20 +2155,26 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
                 if (ni == 0) {
                     if (mi > 0) {  // row block mi landed; mi + 1 may still be in flight
                         if (mi + 1 < 8)
-                            asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+                            asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[mi % 4]));
                         else
-                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[c]));
+                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c][0]), "+v"(a[c][1]), "+v"(xv[mi % 4]));
                     }
                     // issue row block mi + 2 into the slot row block mi - 1 used (its MFMAs are issued)
                     if (mi + 2 < 8 && !(ABL & 4)) {
                         const int c2 = (mi + 2) % 3;
-                        const uint32_t ro = (mi + 2) * 16 * FQ_GROUP;
-                        a[c2][0] = ds_read_b128(ab + a_off0 + ro);
-                        a[c2][1] = ds_read_b128(ab + a_off1 + ro);
-                        xv[c2] = XSF ? ds_read_u16_at<0>(ab + x_off + (mi + 2) * 32) : ds_read_b32_at<0>(ab + x_off + (mi + 2) * 64);
+                        if constexpr (DBG) {  // (this loop is not unrolled in the debug variant: one
+                                              // register-addressed read each, no switch to merge)
+                            const uint32_t ro = (mi + 2) * 16 * FQ_GROUP;
+                            a[c2][0] = ds_read_b128(ab0 + ro);
+                            a[c2][1] = ds_read_b128(ab1 + ro);
+                            xv[(mi + 2) % 4] = XSF ? ds_read_u16(abx + (mi + 2) * 32) : ds_read_b32(abx + (mi + 2) * 64);
+                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c2][0]), "+v"(a[c2][1]), "+v"(xv[(mi + 2) % 4]));
+                        } else {
+                            a[c2][0] = ds_read_b128_k<16 * FQ_GROUP>(ab0, mi + 2);
+                            a[c2][1] = ds_read_b128_k<16 * FQ_GROUP>(ab1, mi + 2);
+                            xv[(mi + 2) % 4] = XSF ? ds_read_u16_k<32>(abx, mi + 2) : ds_read_b32_k<64>(abx, mi + 2);
+                        }
                     }
-                    const uint32_t x2u = __builtin_amdgcn_perm(xv[c], xv[c], 0x01000100u);  // half2(xs, xs)
-                    x2s[mi & 1] = *reinterpret_cast<const __half2 *>(&x2u);
                 }
                 v4i acc;
                 if (ABL & 2) {  // (development: operands kept alive, no MFMA)
@@ -2104,7 +2192,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
             if (j > 0) {
                 const int pj = j - 1;
                 if (ABL & 1)  // (development: accumulators kept alive, no dequant)
-                    asm volatile("" ::"v"(accq[pj & 1]), "v"(x2s[(pj >> 2) & 1]), "v"(wv[pj & 3]));
+                    asm volatile("" ::"v"(accq[pj & 1]), "v"(xv[(pj >> 2) % 4]), "v"(wv[pj & 3]));
                 else
                     dequant(accq[pj & 1], pj >> 2, pj & 3);
             }
@@ -3034,6 +3122,9 @@ static fq_status launch_prefill_u8(const int8_t *xq, const uint16_t *xs, const v
 #ifdef FQ_DEV_ABLATION
     if (const char *e = getenv("FQ_DEV_PF128")) small_tiles = atoi(e) != 0;  // development: force either
 #endif
+    // the 256 x 256 kernel addresses its operands by 32-bit buffer offsets (the activations and the
+    // unpacked weights each below 4 GiB; every LLaMA / OPT prefill shape is far below)
+    if ((uint64_t)M * K >= (1ull << 32) || (uint64_t)NT * (K / FQ_GROUP) * 2048 >= (1ull << 32)) small_tiles = true;
     if (small_tiles) {
         if (acc_dbg)
             hipLaunchKernelGGL((fq_gemm_prefill_kernel<true, 0, true>), dim3((unsigned)nwg), dim3(PF_WAVES * 64), 0, s,

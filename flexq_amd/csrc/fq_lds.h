@@ -60,6 +60,43 @@ __device__ __forceinline__ uint32_t ds_read_u16_at(uint32_t a) {
     return v;
 }
 
+template <int OFF>
+__device__ __forceinline__ uint32_t ds_read_b32_at(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+}
+
+// offset k * STEP for a k that is a constant once the caller's loop is unrolled: the switch folds
+// to one immediate-offset read (no v_add for the address); any other k takes the register form
+#define FQ_DS_READ_K(NAME, T, AT, REG)                                                                  \
+    template <int STEP>                                                                                \
+    __device__ __forceinline__ T NAME(uint32_t a, int k) {                                             \
+        switch (k) {                                                                                   \
+            case 0: return AT<0>(a);                                                                   \
+            case 1: return AT<STEP>(a);                                                                \
+            case 2: return AT<2 * STEP>(a);                                                            \
+            case 3: return AT<3 * STEP>(a);                                                            \
+            case 4: return AT<4 * STEP>(a);                                                            \
+            case 5: return AT<5 * STEP>(a);                                                            \
+            case 6: return AT<6 * STEP>(a);                                                            \
+            case 7: return AT<7 * STEP>(a);                                                            \
+            default: return REG(a + k * STEP);                                                         \
+        }                                                                                              \
+    }
+FQ_DS_READ_K(ds_read_b128_k, v4i, ds_read_b128_at, ds_read_b128)
+FQ_DS_READ_K(ds_read_b32_k, uint32_t, ds_read_b32_at, ds_read_b32)
+FQ_DS_READ_K(ds_read_u16_k, uint32_t, ds_read_u16_at, ds_read_u16)
+#undef FQ_DS_READ_K
+
+// fp16 x2 product w * (x.lo, x.lo): v_pk_mul_f16 with the high lane also reading x's low half
+// (op_sel_hi), i.e. __hmul2(w, half2(x.lo, x.lo)) without the v_perm that builds the pair
+__device__ __forceinline__ uint32_t pk_mul_f16_lo(uint32_t w, uint32_t x) {
+    typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+    const _Float16 xl = __builtin_bit_cast(_Float16, (uint16_t)x);
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2_, w) * h2_{xl, xl});  // (the splat folds into op_sel_hi)
+}
+
 // s_waitcnt vmcnt(BASE + k) for a wave-uniform runtime k (immediates only); vmcnt(0) past 7
 template <int BASE>
 __device__ __forceinline__ void wait_vm_plus(int k) {

@@ -14,6 +14,8 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef int v2i_ __attribute__((ext_vector_type(2)));
 
 template <int MODE, int W>  // 0: MFMA only, 1: 16x16x64 + dequant, 2: 32x32x32 + dequant
 __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float *sink) {
@@ -46,6 +48,10 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
     long long t0 = clock64();
     for (int it = 0; it < iters; it++) {
         asm volatile("" : "+v"(a[0][0]), "+v"(b[0][0]), "+v"(xv[0]), "+v"(wv[0][0]));
+        if (MODE >= 10) {  // every scale operand loop-variant (nothing hoisted out of the loop)
+#pragma unroll
+            for (int i = 0; i < 4; i++) asm volatile("" : "+v"(xv[i]), "+v"(wv[i][0]), "+v"(wv[i][1]));
+        }
         if (MODE == 0) {
 #pragma unroll
             for (int mi = 0; mi < 4; mi++)
@@ -55,7 +61,7 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
                     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
                     out[mi][ni][0] += __int_as_float(acc[0] ^ acc[3]);
                 }
-        } else if (MODE == 1) {
+        } else if (MODE == 1 || MODE == 13) {
 #pragma unroll
             for (int mi = 0; mi < 4; mi++) {
                 const uint32_t x2u = __builtin_amdgcn_perm(xv[mi], xv[mi], 0x01000100u);
@@ -94,6 +100,54 @@ __global__ __launch_bounds__(64 * W) void kern(int iters, long long *cyc, float 
                     o[1] = fmaf(__int_as_float(acc[1]) - 12582912.0f, __high2float(p01), o[1]);
                     o[2] = fmaf(__int_as_float(acc[2]) - 12582912.0f, __low2float(p23), o[2]);
                     o[3] = fmaf(__int_as_float(acc[3]) - 12582912.0f, __high2float(p23), o[3]);
+                }
+            }
+        } else if (MODE == 11 || MODE == 12) {
+            // 11: mode 10 with the bias removed by packed v_pk_add_f32 (two outputs per instruction):
+            // per 16x16 block 2 pk_add + 2 pk_mul + 4 fma_mix = 4 VALU per MFMA instead of 5.
+            // 12: the same, software-pipelined as mode 6 (block b's MFMAs, then block b - 1's dequant)
+            const int B = 0x4B400000;
+            const v2f nb = v2f{-12582912.0f, -12582912.0f};
+            auto deq = [&](const v4i acc, int pm, int pn) {
+                const uint32_t x2u = __builtin_amdgcn_perm(xv[pm], xv[pm], 0x01000100u);
+                const __half2 x2 = *reinterpret_cast<const __half2 *>(&x2u);
+                const uint32_t w01 = wv[pn][0], w23 = wv[pn][1];
+                const __half2 p01 = __hmul2(*reinterpret_cast<const __half2 *>(&w01), x2);
+                const __half2 p23 = __hmul2(*reinterpret_cast<const __half2 *>(&w23), x2);
+                v2f f01 = __builtin_bit_cast(v2f, v2i_{acc[0], acc[1]});
+                v2f f23 = __builtin_bit_cast(v2f, v2i_{acc[2], acc[3]});
+                asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(f01) : "v"(nb));
+                asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(f23) : "v"(nb));
+                float *o = out[pm][pn];
+                const uint32_t q01 = __builtin_bit_cast(uint32_t, p01), q23 = __builtin_bit_cast(uint32_t, p23);
+                asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[0,1,0]" : "+v"(o[0]) : "v"(f01[0]), "v"(q01));
+                asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "+v"(o[1]) : "v"(f01[1]), "v"(q01));
+                asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[0,1,0]" : "+v"(o[2]) : "v"(f23[0]), "v"(q23));
+                asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "+v"(o[3]) : "v"(f23[1]), "v"(q23));
+            };
+            if (MODE == 11) {
+#pragma unroll
+                for (int mi = 0; mi < 4; mi++)
+#pragma unroll
+                    for (int ni = 0; ni < 4; ni++) {
+                        v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{B, B, B, B}, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], acc, 0, 0, 0);
+                        deq(acc, mi, ni);
+                    }
+            } else {
+                v4i accs[2];
+                accs[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[0][0], a[0][0], v4i{B, B, B, B}, 0, 0, 0);
+                accs[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[0][1], a[0][1], accs[0], 0, 0, 0);
+#pragma unroll
+                for (int bl = 1; bl <= 16; bl++) {
+                    const int mi = bl >> 2, ni = bl & 3;
+                    if (bl < 16) {
+                        accs[bl & 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][0], a[mi][0], v4i{B, B, B, B}, 0, 0, 0);
+                        accs[bl & 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[ni][1], a[mi][1], accs[bl & 1], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    deq(accs[(bl - 1) & 1], (bl - 1) >> 2, (bl - 1) & 3);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
         } else if (MODE == 8 || MODE == 9) {
@@ -297,6 +351,19 @@ int main() {
     run<1, 4>("16x16x64 + dequant");
     run<10, 8>("16x16x64 biased + sub");
     run<10, 4>("16x16x64 biased + sub");
+    if (getenv("UBD_PK_ONLY")) {
+        run<1, 8>("16x16x64 + dequant");
+        run<13, 8>("16x16x64 + dequant, no hoist");
+        run<10, 8>("16x16x64 biased + sub");
+        run<11, 8>("16x16x64 biased + pk_add");
+        run<12, 8>("16x16x64 biased + pk_add, pipelined");
+        run<6, 8>("16x16 pipelined");
+        run<1, 4>("16x16x64 + dequant");
+        run<11, 4>("16x16x64 biased + pk_add");
+        run<12, 4>("16x16x64 biased + pk_add, pipelined");
+        run<0, 8>("mfma only 16x16x64");
+        return 0;
+    }
     if (getenv("UBD_BF16_ONLY")) return 0;
     run<6, 4>("16x16 pipelined");
     run<7, 4>("32x32 pipelined");
