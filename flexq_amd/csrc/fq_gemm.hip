@@ -2585,7 +2585,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         return FQ_ERR_SHAPE;  // (never for the planner's decode plans; the packing's bounds)
     const void *xarg = FUSE ? (const void *)a.xh : (const void *)a.xq;
 #ifdef FQ_DEV_ABLATION
-    if (!DBG && !CH && MT == 4 && XS == 0 && SS == 0) {  // (the fused and the unfused kernel)
+    if (!DBG && !CH && (MT == 4 || MT == 16) && XS == 0 && SS == 0) {  // (the fused and the unfused kernel)
         const int abl = dev_ablation();
 #define FQ_ABL(v)                                                                                           \
     if (abl == v) {                                                                                           \

@@ -1,7 +1,8 @@
 """Decode-kernel timeline (development tool; tools/libflexq_hip_abl.so, ablation mask 16).
 Per workgroup s_memrealtime stamps (100 MHz): 0 entry, 1 ring prologue issued, 2 first block
 landed, 3 item loop done, 4 split-K fix-up done.  Prints, per shape, the kernel span against the
-graph-replay time per launch, the dispatch skew and the phase medians (us)."""
+graph-replay time per launch, the dispatch skew and the phase medians (us).  FQ_STAMP_M: rows (default
+1; 16 stamps the batch-16 GEMM); FQ_STAMP_SHAPES: "N K N K ..." instead of the default shapes."""
 import ctypes
 import os
 import sys
@@ -23,19 +24,24 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     R, COPIES = 20, 6
+    M = int(os.environ.get("FQ_STAMP_M", "1"))
+    shapes = SHAPES
+    if os.environ.get("FQ_STAMP_SHAPES"):
+        a = [int(v) for v in os.environ["FQ_STAMP_SHAPES"].split()]
+        shapes = list(zip(a[0::2], a[1::2]))
     os.environ["FQ_DEV_ABLATION"] = os.environ.get("FQ_STAMP_MASK", "16")
     L = _lib.load()
     L.fq_dev_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     stream = torch.cuda.Stream()
     for linear in (False, True):
-        for (N, K) in SHAPES:
+        for (N, K) in shapes:
             copies = []
             for _ in range(COPIES):
                 wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
                 copies.append(ops.pack_w6(wq, (torch.rand((K // 128, N), device=dev, generator=g) * 0.01).half()))
-            x = torch.randn((1, K), device=dev, dtype=torch.float16, generator=g)
+            x = torch.randn((M, K), device=dev, dtype=torch.float16, generator=g)
             xq, xs = ops.quantize_act(x, 6)
-            out = torch.empty((1, N), device=dev, dtype=torch.float16)
+            out = torch.empty((M, N), device=dev, dtype=torch.float16)
 
             def run(c):
                 if linear:
@@ -69,7 +75,7 @@ def main():
             t0 = st[:, 0].min()
             us = lambda v: v / 100.0  # 100 MHz ticks -> us
             end = np.maximum(st[:, 3], st[:, 4])
-            print(f"{'linear' if linear else 'gemm  '} N={N:6d} K={K:6d} wgs={len(st):4d} per_launch={per:6.2f} "
+            print(f"{'linear' if linear else 'gemm  '} M={M} N={N:6d} K={K:6d} wgs={len(st):4d} per_launch={per:6.2f} "
                   f"span={us(end.max() - t0):6.2f} skew={us(st[:, 0].max() - t0):5.2f} "
                   f"stage={us(np.median(st[:, 7] - st[:, 0])):5.2f} issue={us(np.median(st[:, 1] - st[:, 0])):5.2f} first={us(np.median(st[:, 2] - st[:, 1])):5.2f} "
                   f"loop={us(np.median(st[:, 3] - st[:, 2])):6.2f} (max {us((st[:, 3] - st[:, 2]).max()):6.2f}) "
