@@ -649,6 +649,14 @@ __device__ __forceinline__ void decode_body(
         }
     };
 
+    // buffer resources of the activation codes, their scales and the image's w-scales (issue, stage_all)
+    const __amdgpu_buffer_rsrc_t xqr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)xq, (short)0, (int)((uint32_t)M * (uint32_t)K), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xsr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)xs, (short)0, (int)((uint32_t)G * (uint32_t)ldx * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wsr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)wsb, (short)0, (int)((uint32_t)NT * G * 32), 0x00020000);
+
     // ---- staging of the wave's scales (and unfused activation rows): issued right after the
     // first ring block (below), so that every wave's first-needed DMAs leave the CU's address unit
     // before the rest of the prologue burst; the first ring wait retires it in order.
@@ -669,12 +677,23 @@ __device__ __forceinline__ void decode_body(
             }
         }
         if (n > 0 && !XS && !FUSE && !(ABL & 8)) {  // activation rows: 8 lanes x 16 B per (group, row)
+            // the lane's pair rg = r0 + lane / 8 as (group j, row), stepped without a division per piece
+            int j = 0, row = lane >> 3;
+            while (row >= M) {
+                row -= M;
+                ++j;
+            }
             for (int r0 = 0; r0 < R; r0 += 8) {
-                const int rg = r0 + (lane >> 3) < R ? r0 + (lane >> 3) : R - 1;
-                const int j = rg / M, row = rg - j * M;
-                const int chunk = (lane & 7) ^ (row & 7);  // lands at position lane & 7 (xswz)
-                __builtin_amdgcn_global_load_lds(xq + (long)row * K + (long)(ga + j) * FQ_GROUP + chunk * 16,
-                                                 LDS_PTR(x_st + r0 * 128), 16, 0, 0);
+                const bool in = r0 + (lane >> 3) < R;  // past the last pair: a copy of pair R - 1
+                const int jj = in ? j : ng - 1, rw = in ? row : M - 1;
+                const int chunk = (lane & 7) ^ (rw & 7);  // lands at position lane & 7 (xswz)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xqr, LDS_PTR(x_st + r0 * 128), 16,
+                                                         (uint32_t)rw * K + (uint32_t)(ga + jj) * FQ_GROUP + chunk * 16, 0, 0, 0);
+                row += 8;
+                while (row >= M) {
+                    row -= M;
+                    ++j;
+                }
             }
         }
         FQ_STAMP(7);
@@ -689,31 +708,35 @@ __device__ __forceinline__ void decode_body(
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, (int)((uint32_t)NT * G * FQ_BLOCK), 0x00020000);
     const uint32_t wvo = lane * 16;
-    uint32_t roff = ((uint32_t)t0 * G + ga) * FQ_BLOCK;                 // next block to issue (V2)
+    uint32_t roff = ((uint32_t)t0 * G + ga) * FQ_BLOCK;                 // next block to issue
     const uint32_t rjump = ((uint32_t)tstep * G - ng + 1) * FQ_BLOCK;  // an item's last group -> the next item's first
-    const char *wbytes = reinterpret_cast<const char *>(wpk) + lane * 16;
+    // Every DMA of the ring and the staging goes through a buffer resource with a per-lane offset fixed
+    // for the launch and the block / group in an SGPR offset (never the instruction's immediate: on an
+    // LDS-DMA it moves the LDS destination too), so the unfused variants' refills carry no 64-bit
+    // address VALU either (the host keeps the image < 4 GiB; M x K, scales smaller still).
+    uint32_t xpo[C::XP > 0 ? C::XP : 1];  // XS: the lane's activation piece offsets (row, swizzled chunk)
+#pragma unroll
+    for (int p = 0; p < C::XP; p++) {
+        const int row = p * 8 + (lane >> 3), chunk = (lane & 7) ^ (row & 7);
+        xpo[p] = (uint32_t)(row < M ? row : M - 1) * (uint32_t)K + chunk * 16;
+    }
     auto issue = [&](int it, int j, int slot) {  // block (item it, group ga + j) -> slot
         const int t = item_tile(it), g = ga + j;
         char *dst = ring + slot * C::SLOT;
-        if constexpr (V2) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst), 16, wvo, roff, 0, FQ_W_AUX);
-            if (lane < 32) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + 1024), 16, wvo, roff + 1024, 0, FQ_W_AUX);
-            return;
-        }
-        const char *src = wbytes + ((long)t * G + g) * FQ_BLOCK;
-        __builtin_amdgcn_global_load_lds(src, LDS_PTR(dst), 16, 0, FQ_W_AUX);
-        if (lane < 32) __builtin_amdgcn_global_load_lds(src + 1024, LDS_PTR(dst + 1024), 16, 0, FQ_W_AUX);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst), 16, wvo, roff, 0, FQ_W_AUX);
+        if (lane < 32) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(dst + 1024), 16, wvo, roff + 1024, 0, FQ_W_AUX);
+        if constexpr (V2) return;
 #pragma unroll
-        for (int p = 0; p < C::XP; p++) {  // activation rows [MT][128 B], swizzled chunks
-            const int row = p * 8 + (lane >> 3), chunk = (lane & 7) ^ (row & 7);
-            __builtin_amdgcn_global_load_lds(xq + (long)(row < M ? row : M - 1) * K + (long)g * FQ_GROUP + chunk * 16,
-                                             LDS_PTR(dst + FQ_BLOCK + p * 1024), 16, 0, 0);
-        }
+        for (int p = 0; p < C::XP; p++)  // activation rows [MT][128 B], swizzled chunks
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xqr, LDS_PTR(dst + FQ_BLOCK + p * 1024), 16, xpo[p],
+                                                     (uint32_t)g * FQ_GROUP, 0, 0);
         if (SS) {  // 16 w-scales (16 B per lane, lanes 0..1) and XSR x-scales (ushort, lanes 0..XSR-1)
             if (lane < 2)
-                __builtin_amdgcn_global_load_lds(wsb + ((long)t * G + g) * 16 + 8 * lane, LDS_PTR(dst + C::WS_OFF), 16, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wsr, LDS_PTR(dst + C::WS_OFF), 16, 16 * lane,
+                                                         ((uint32_t)t * G + g) * 32, 0, 0);
             if (lane < XSR)
-                __builtin_amdgcn_global_load_lds(xs + (long)g * ldx + (lane < M ? lane : M - 1), LDS_PTR(dst + C::XS_OFF), 2, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xsr, LDS_PTR(dst + C::XS_OFF), 2, (uint32_t)(lane < M ? lane : M - 1) * 2,
+                                                         (uint32_t)g * ldx * 2, 0, 0);
         }
     };
     // Order: first activation window -> ring block 0 -> staging -> ring blocks 1 .. D-1 (exactly
@@ -1198,9 +1221,12 @@ __device__ __forceinline__ void decode_body(
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
+            // (k = e / EM by a multiply-high with ceil(2^32 / EM): exact while e * EM < 2^32 -- e < IPW * EM
+            // with IPW <= 4096 and EM <= 512 -- instead of a per-element integer division)
+            const uint32_t emi = (uint32_t)(0xffffffffu / (uint32_t)EM) + 1u;
             if ((GAT || CHN) && S == 1) {  // peer-store gather / chain: two adjacent columns per thread
                 for (int e = 2 * threadIdx.x; e < (rs + 1) * EM; e += 2 * NW * 64) {
-                    const int k = e / EM, ee = e - k * EM;
+                    const int k = (int)(((uint64_t)(uint32_t)e * emi) >> 32), ee = e - k * EM;
                     float v0 = 0.f, v1 = 0.f;
 #pragma unroll
                     for (int w = 0; w < NW; w++) {
@@ -1215,7 +1241,7 @@ __device__ __forceinline__ void decode_body(
                 }
             } else
             for (int e = threadIdx.x; e < (rs + 1) * EM; e += NW * 64) {
-                const int k = e / EM, ee = e - k * EM;
+                const int k = (int)(((uint64_t)(uint32_t)e * emi) >> 32), ee = e - k * EM;
                 float v = 0.f;
 #pragma unroll
                 for (int w = 0; w < NW; w++) v += red[(k * NW + w) * EM + ee];
@@ -2607,7 +2633,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
-    if constexpr (PRO != 0) {  // the fused producers (FUSE, S as planned, no debug output, no gather)
+    if constexpr (PRO != 0 && PRO != 4) {  // the fused producers (FUSE, S as planned, no debug output, no gather)
         if (p.NCH != 1) return FQ_ERR_SHAPE;  // (the producer plans have one row chunk)
         hipLaunchKernelGGL((fq_gemm_decode_pro_kernel<MT, PRO>), grid, block, lds, stream, a.xh,
                            (const uint32_t *)a.wpk, a.pro.in, a.pro.gamma, pk.w0, pk.w1, pk.w2, pk.w3, a.pro.ldh,
