@@ -1,8 +1,9 @@
 """Decode-chain timeline (development tool; tools/libflexq_hip_abl.so).  Runs the bench's layer
 chain (o -> gate_up -> down -> qkv, LLaMA-2-7B, M = 1, each input the leading K values of the previous
 output) in a graph, then reads the per-(WG, linear) wave-0 stamps (s_memrealtime, 100 MHz): 0 linear
-start, 1 ring issued, 2 input quantized (after the in-kernel wait), 3 first block landed, 4 stream
-done, 5 linear end.  Prints, per linear, medians and spreads over the WGs (us, from the launch's
+start, 1 ring issued (a linear after the first: its prologue; the ring itself went out from the
+previous linear's tail, stamp 7 there), 2 input quantized (after the in-kernel wait), 3 first block
+landed, 4 stream done (its output granules stored), 5 linear end, 6 the poll's first pass matched.  Prints, per linear, medians and spreads over the WGs (us, from the launch's
 first stamp) and the hand-off: from the last WG's stream end of linear l to each WG's input-ready
 time of linear l + 1.  FQ_STAMPS_PRO=1: the decoder layer's producer chain instead (o -> RMSNorm +
 gate_up -> SiLU * up + down -> RMSNorm + qkv, layers.run_layers_chained's links)."""
@@ -83,6 +84,14 @@ def main():
               f"input quantized median {np.median(ready) - last:+.2f} [{ready.min() - last:+.2f} .. {ready.max() - last:+.2f}] us; "
               f"consumer first block {np.median(us[:, li, 3]) - last:+.2f}; ring issued (median) {np.median(us[:, li, 1]) - last:+.2f}")
     print("launch span", f"{us[:, len(SHAPES) - 1, 5].max():.2f} us")
+    if not os.environ.get("FQ_STAMPS_PRO"):  # plain chain: 6 = the first poll pass matched, 7 = next ring issued (tail)
+        for li in range(1, len(SHAPES)):
+            last = us[:, li - 1, 4].max()
+            tail = us[:, li - 1, 7]
+            print(f"edge {SHAPES[li - 1][0]} -> {SHAPES[li][0]}: last producer stream done {last:7.2f}; next ring issued "
+                  f"(tail) median {np.median(tail) - last:+.2f}; consumer poll done median {np.median(us[:, li, 6]) - last:+.2f} "
+                  f"[{us[:, li, 6].min() - last:+.2f} .. {us[:, li, 6].max() - last:+.2f}]; input quantized "
+                  f"{np.median(us[:, li, 2]) - last:+.2f}; first block {np.median(us[:, li, 3]) - last:+.2f} us")
     if os.environ.get("FQ_STAMPS_PRO"):  # 6: both sources arrived (poll done), 7: RMSNorm's barrier passed
         for li in range(1, len(SHAPES)):
             p6, p7 = us[:, li, 6], us[:, li, 7]
