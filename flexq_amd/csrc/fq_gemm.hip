@@ -873,6 +873,7 @@ __device__ __forceinline__ void decode_body(
                         if (lane == 0) chain_fail(pro.chain);
                     }
                 }
+                if (c == 0) FQ_CSTAMP(6);  // (development stamps: the first pass's tags all matched)
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1267,7 +1268,10 @@ __device__ __forceinline__ void decode_body(
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         FQ_CSTAMP(5);
-        if (FQ_CHAIN_AHEAD && pro.nxt_w) chain_ring_ahead<MT>(pro.nxt_w, pro.nxt_p);
+        if (FQ_CHAIN_AHEAD && pro.nxt_w) {
+            chain_ring_ahead<MT>(pro.nxt_w, pro.nxt_p);
+            if (!CHP) FQ_CSTAMP(7);  // (development stamps: the next linear's ring issued)
+        }
         return;
     }
     // GAT is a separate instantiation: the gather's branches and publish step cost the plain
