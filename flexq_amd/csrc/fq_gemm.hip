@@ -2000,7 +2000,7 @@ __device__ unsigned long long g_pb_stamps[256 * PB_WAVES * 4];
 #define PB_STAMP(k)
 #endif
 
-// ABL: development ablations as in fq_gemm_prefill_kernel (1, 2, 4, 8, 16; 32 stamps).  XSF (M % 256 == 0:
+// ABL: development ablations as in fq_gemm_prefill_kernel (1, 2, 4, 8, 16; 32 stamps; 64 no priority).  XSF (M % 256 == 0:
 // every row tile full, its x-scales 16-byte aligned): the 256 x-scales of a group arrive packed in
 // one 512-byte DMA piece instead of four 64-lane ushort pieces into dword slots.
 // QO: the epilogue also quantizes the fp16 output for the next linear (PbQ; N % 128 == 0): a tile
@@ -2039,7 +2039,7 @@ __global__ __launch_bounds__(PB_WAVES * 64, 1) void fq_gemm_prefill_big_kernel(
     const bool dmaw = wid >= 4;
     // Static priority for the DMA waves (measured: -2..-5 % against none or waves 0-3 prioritised):
     // their next stage leaves earlier, and they are the later-dispatched, arbitration-losing half.
-    if (dmaw) __builtin_amdgcn_s_setprio(1);
+    if (dmaw && !(ABL & 64)) __builtin_amdgcn_s_setprio(1);  // (ABL & 64: development, no priority)
     const int v4 = wid & 3;
     const int swz = ((lane & 7) ^ ((lane >> 3) & 7)) * 16;  // (row & 7 == (lane >> 3) & 7 for all 8 pieces)
     const int srow = 64 * v4 + lane;
@@ -3226,7 +3226,7 @@ fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_
         FQ_LAUNCH_CHECK();
         return FQ_OK;
     }
-    if (!acc_dbg && dev_ablation() >= 129 && dev_ablation() <= 191 && M >= PF_U8_MIN_M && workspace &&
+    if (!acc_dbg && dev_ablation() >= 128 && dev_ablation() <= 255 && M >= PF_U8_MIN_M && workspace &&
         workspace_bytes >= kTicketBytes + prefill_u8_bytes(N, K)) {  // the 256 x 256 kernel, ABL = value - 128
         const int abl = dev_ablation() - 128;
         char *wu = (char *)workspace + kTicketBytes;
@@ -3239,7 +3239,8 @@ fq_status fq_gemm_w6ax_impl(const int8_t *xq, const uint16_t *xs, const void *w_
         if (abl == v)                                                                                        \
             hipLaunchKernelGGL((fq_gemm_prefill_big_kernel<false, v>), dim3(nbig), dim3(PB_WAVES * 64), lds_big, s, \
                                xq, xs, (const uint32_t *)w_packed, M, N, K, d, acc_dbg, (const char *)wu, PbQ{});
-        FQ_BABL(1) FQ_BABL(2) FQ_BABL(3) FQ_BABL(4) FQ_BABL(8) FQ_BABL(12) FQ_BABL(16) FQ_BABL(7) FQ_BABL(15) FQ_BABL(32)
+        FQ_BABL(0) FQ_BABL(1) FQ_BABL(2) FQ_BABL(3) FQ_BABL(4) FQ_BABL(8) FQ_BABL(12) FQ_BABL(16) FQ_BABL(7) FQ_BABL(15) FQ_BABL(32) \
+        FQ_BABL(33) FQ_BABL(34) FQ_BABL(35) FQ_BABL(36) FQ_BABL(40) FQ_BABL(64) FQ_BABL(96) FQ_BABL(104)
 #undef FQ_BABL
         FQ_LAUNCH_CHECK();
         return FQ_OK;

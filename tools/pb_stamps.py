@@ -4,7 +4,8 @@ s_memtime sums of four segments of every group step: the barrier wait, the stage
 4-7 issue it all), the compute (LDS reads, MFMAs, dequant) and the trailing wait for the next
 stage.  Prints cycles per group step by wave, averaged over the workgroups.  The stamps fence the
 segments (no overlap across them), so read the shares, not the total.
-usage: python tools/pb_stamps.py [M N K]"""
+usage: python tools/pb_stamps.py [M N K]   (FQ_PB_ABL=1|2|4|8: stamps of an ablated build -- no dequant,
+no MFMA, no LDS fragment reads, no DMA)"""
 import ctypes
 import os
 import sys
@@ -24,7 +25,8 @@ def main():
     M, N, K = (int(v) for v in sys.argv[1:4]) if len(sys.argv) > 3 else (16384, 28672, 4096)
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    os.environ["FQ_DEV_ABLATION"] = "160"
+    abl = int(os.environ.get("FQ_PB_ABL", "0"))
+    os.environ["FQ_DEV_ABLATION"] = str(160 + abl)
     L = _lib.load()
     L.fq_dev_pb_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
@@ -39,7 +41,7 @@ def main():
     L.fq_dev_pb_stamps(buf.ctypes.data, buf.size)
     st = buf.reshape(256, 8, 4).astype(np.float64) / (K // 128)
     names = ["barrier", "stage-issue", "compute", "dma-wait"]
-    print(f"M={M} N={N} K={K}: s_memtime cycles per group step (mean over 256 WGs)")
+    print(f"M={M} N={N} K={K} ablation={abl}: s_memtime cycles per group step (mean over 256 WGs)")
     for w in range(8):
         row = " ".join(f"{names[k]}={st[:, w, k].mean():7.0f}" for k in range(4))
         print(f"  wave {w}: {row}  total={st[:, w, :].sum(axis=1).mean():7.0f}")
