@@ -84,6 +84,17 @@ def main():
               f"input quantized median {np.median(ready) - last:+.2f} [{ready.min() - last:+.2f} .. {ready.max() - last:+.2f}] us; "
               f"consumer first block {np.median(us[:, li, 3]) - last:+.2f}; ring issued (median) {np.median(us[:, li, 1]) - last:+.2f}")
     print("launch span", f"{us[:, len(SHAPES) - 1, 5].max():.2f} us")
+    # the workgroups holding an extra tile of the widest link (bid < N_tiles % grid) against the rest
+    wide = max(range(len(SHAPES)), key=lambda li: SHAPES[li][1])
+    ir = ((SHAPES[wide][1] + 15) // 16) % 256
+    if ir:
+        print(f"by workgroup: bid < {ir} (an extra {SHAPES[wide][0]} tile) vs the rest, medians (us)")
+        for li, (name, N, K, _) in enumerate(SHAPES):
+            row = "  ".join(f"{nm} {np.median(us[:ir, li, k]):7.2f} / {np.median(us[ir:, li, k]):7.2f}"
+                            for k, nm in enumerate(names) if k in (0, 3, 4))
+            print(f"{name:8s} {row}")
+    if os.environ.get("FQ_STAMPS_RAW"):
+        np.save(os.environ["FQ_STAMPS_RAW"], us)
     if not os.environ.get("FQ_STAMPS_PRO"):  # plain chain: 6 = the first poll pass matched, 7 = next ring issued (tail)
         for li in range(1, len(SHAPES)):
             last = us[:, li - 1, 4].max()
