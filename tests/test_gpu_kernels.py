@@ -662,6 +662,9 @@ def test_prefill_quantized_output_bit_identical(ops, dev, M, N, K, qM, qK, qbits
     pytest.param(16384, 6144, 4096, 8, True, marks=pytest.mark.timeout(300)),    # qkv (GQA)
     pytest.param(16384, 28672, 4096, 8, True, marks=pytest.mark.timeout(300)),   # gate_up merged
     pytest.param(16384, 4096, 14336, 8, True, marks=pytest.mark.timeout(300)),   # down_proj: 112 groups
+    # activation codes just past 4 GiB (M x K > 2^32): the host leaves the buffer-addressed 256 x 256
+    # kernel (32-bit offsets) for the 128 x 128 one with 64-bit addresses (launch_prefill_u8)
+    pytest.param((1 << 20) + 64, 256, 4096, 8, False, marks=pytest.mark.timeout(300)),
 ])
 def test_gemm_prefill_sampled(ops, dev, M, N, K, abits, with_acc):
     """Prefill sizes: the whole GEMM on the GPU, the oracle on a seeded sample of rows x columns."""
@@ -686,6 +689,23 @@ def test_gemm_prefill_sampled(ops, dev, M, N, K, abits, with_acc):
         np.testing.assert_array_equal(host(acc.index_select(0, rows_t).index_select(1, cols_t)), acc_ref)
     assert_gemm_close(host(d.index_select(0, rows_t).index_select(1, cols_t)), ref, mag,
                       f"prefill M={M} N={N} K={K}")
+
+
+@pytest.mark.timeout(300)
+def test_quantize_act_past_4g_elements(ops, dev):
+    """fq_quantize_act over M x K > 2^32 elements (its 64-bit index form): sampled rows bit-exact
+    against the oracle, the rows on both sides of element 2^32 included."""
+    M, K = (1 << 20) + 64, 4096
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn((M, K), device=dev, dtype=torch.float16, generator=g)
+    xq, xs = ops.quantize_act(x, 8)
+    edge = (1 << 32) // K
+    rows = torch.tensor([0, 1, edge - 1, edge, edge + 1, M - 2, M - 1], device=dev)
+    q_ref, s_ref = oracle.quantize_engine(host(x.index_select(0, rows)), 8)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(xq.index_select(0, rows)), q_ref)
+    np.testing.assert_array_equal(host(xs.index_select(1, rows)).view(np.uint16), s_ref.view(np.uint16))
+    del x, xq, xs
 
 
 def test_workspace_growth_is_geometric(ops, dev):
