@@ -57,6 +57,18 @@ def test_null_and_shape_errors_are_status_codes():
     assert lib.fq_quantize_act(P(16), 1, 100, 6, P(16), P(16), None) == 2      # K % 128
     assert lib.fq_quantize_act(P(16), 1, 128, 7, P(16), P(16), None) == 3      # bits
     assert lib.fq_ref_bit_packing(P(16), P(16), 12, 128, 6, None) == 2         # rows 9..15 unsupported
+    # the GEMM and the linear: empty or ragged-K shapes, bad bits and null operands are status codes,
+    # checked before any device call (an empty M, N or K is FQ_ERR_SHAPE, never an empty launch)
+    g = lambda M, N, K, b=6, d=P(16): lib.fq_gemm_w6ax(P(16), P(16), P(16), M, N, K, b, d,  # noqa: E731
+                                                        None, None, 0, None)
+    assert g(1, 4096, 4096, d=None) == 1
+    assert [g(0, 4096, 4096), g(1, 0, 4096), g(1, 4096, 0), g(1, 4096, 100), g(-1, 4096, 4096)] == [2] * 5
+    assert g(1, 1 << 21, 4096) == 2                                              # tiles past the ticket region
+    assert g(1, 4096, 4096, b=7) == 3
+    ln = lambda M, N, K, b=6: lib.fq_linear_w6ax(P(16), M, N, K, b, P(16), P(16), P(16), None, None, 0,  # noqa: E731
+                                                 None)
+    assert [ln(0, 4096, 4096), ln(1, 0, 4096), ln(1, 4096, 0), ln(1, 4096, 200)] == [2] * 4
+    assert ln(1, 4096, 4096, b=4) == 3
 
 
 def test_missing_extension_fails_loudly():
