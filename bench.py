@@ -513,6 +513,8 @@ def cpu_baseline(budget_s=15.0, lins=None, M=1):
 LINE_MAX = 6000
 ESSENTIAL = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+# N > 1: the same workload's one-GPU point and the collectives' world / backend, never dropped either
+KEEP = ESSENTIAL + ("same_workload_1gpu", "comm")
 # optional sections, dropped from the line in this order while it is too long (all stay in the detail file)
 DROP_ORDER = ("vs_reference_sweep", "decoder_layers_e2e", "tp_llama2_7b_peer_gather", "tp_peer_gather",
               "c4_llama2_70b_tp_peer_gather", "replicas", "vs_rocblas_fp16", "tp_llama2_7b", "c4_llama2_70b_tp",
@@ -562,7 +564,7 @@ def compact_line(res, detail=None, limit=LINE_MAX):
         if k in out:
             out[k] = "in detail_file"
     if len(json.dumps(out)) > limit:  # last resort: the essentials alone
-        out = {k: out[k] for k in ESSENTIAL if k in out}
+        out = {k: out[k] for k in KEEP if k in out}
         if detail:
             out["detail_file"] = detail
     return out
@@ -738,6 +740,44 @@ def measure_tp(ctx, cfg, merge, tp, steps, warmup, peer=False):
                                                                    for (_, N, K, _) in launch_lins)),
                 launches_per_step=n_lin, fused_launches=all(fused.values()), graph=use_graph, finite=finite,
                 final=final)
+
+
+def measure_alone(ctx, cfg, merge, steps, warmup):
+    """The same workload on ONE GPU, measured inside an N-rank run: rank 0 builds the
+    whole (unsharded) stack and times it as one HIP graph of its per-linear launches -- the form the
+    column-parallel step runs on every rank, minus the split and the gathers -- while the other ranks wait;
+    ms per step broadcast to every rank.  The denominator of the line's strong-scaling efficiency, taken on
+    the same node and in the same run as the split it is compared with."""
+    layers, M, lins, _ = cfg
+    ms = torch.zeros(1, dtype=torch.float64, device=ctx.dev)
+    if ctx.rank == 0:
+        stack = build_stack(cfg, 0, 1, ctx.dev, merge)
+        step = lambda: run_step(stack, M, 1)  # noqa: E731
+        with torch.cuda.stream(ctx.stream):
+            step()
+        torch.cuda.synchronize()
+        g = capture(step, ctx.stream) if not ctx.a.no_graph else None
+        with torch.cuda.stream(ctx.stream):
+            for _ in range(warmup):
+                g.replay() if g is not None else step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(ctx.stream):
+            for _ in range(steps):
+                g.replay() if g is not None else step()
+        torch.cuda.synchronize()
+        ms[0] = (time.perf_counter() - t0) / steps * 1e3
+        del stack, g
+        torch.cuda.empty_cache()
+    if ctx.world > 1:
+        dist.broadcast(ms, src=0)  # (the other ranks wait here while rank 0 measures)
+    return float(ms.item())
+
+
+def scaling_vs_1gpu(ms_n, ms_1, world, what):
+    """Strong scaling against the same workload on one GPU: speedup ms_1 / ms_N, efficiency / N."""
+    return {"what": what, "ms_per_step_1gpu": round(ms_1, 4), "ms_per_step": round(ms_n, 4),
+            "speedup_vs_1gpu": round(ms_1 / ms_n, 4), "strong_scaling_efficiency": round(ms_1 / ms_n / world, 4)}
 
 
 def measure_single(ctx, name, merge, steps, warmup):
@@ -1180,6 +1220,18 @@ def main():
         res["decode_chain"] = chain_sec
     if staged:
         res["rehearsal"] = "--share-gpu: all ranks on one GPU, gloo with host-staged gathers (not a valid result)"
+    if world > 1:  # what the collectives actually ran on
+        res["comm"] = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                       "rccl_version": ".".join(str(v) for v in torch.cuda.nccl.version())
+                       if dist.get_backend() == "nccl" else None}
+    if tp > 1:  # the same workload on one GPU, same node, same run: the curve's like-for-like point
+        def same_1gpu():
+            ms1 = measure_alone(ctx, hcfg, merge, max(2, a.steps // 2), max(1, a.warmup // 2))
+            return scaling_vs_1gpu(elapsed / a.steps * 1e3, ms1, world,
+                                   f"`value`'s workload ({'C4' if c4_head else a.config}) unsharded on one GPU "
+                                   "(rank 0 alone, per-linear launches in one graph) vs its column split over the "
+                                   f"{world} GPUs; vs_baseline stays null (BASELINE.md publishes no number)")
+        optional(res, "same_workload_1gpu", same_1gpu, ctx)  # (rank 0 alone holds the unsharded weights)
     if prefill and tp == 1:
         ach = ops_launch / per_gemm_s / 1e12
         bytes_pf = int(layers * sum(alg_bytes(M, N, K, ab, False) for (_, N, K, ab) in launch_lins) / n_lin)
@@ -1210,11 +1262,14 @@ def main():
         # linear column-parallel over the N GPUs + one RCCL all-gather per linear (strong scaling)
         def tp_rccl():
             rr = measure_tp(ctx, cfg, merge, world, a.steps, a.warmup)
+            ms1 = measure_alone(ctx, cfg, merge, max(2, a.steps // 2), max(1, a.warmup // 2))
+            sc = scaling_vs_1gpu(rr["ms_per_step"], ms1, world, "")
             return {"what": f"tp{world}: the same stack, every linear column-parallel (N/{world} rows per rank) "
                             "+ one RCCL all_gather_into_tensor of its fp16 output per linear (strong scaling)",
                     "value": round(rr["flops_step"] * a.steps / rr["elapsed"] / 1e12, 4), "unit": "TFLOPS-equiv",
                     "tok_per_s": round(M * a.steps / rr["elapsed"], 2), **tp_summary(rr),
-                    "finite": rr["finite"], "hbm_frac_per_rank": round(rr["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4)}
+                    "finite": rr["finite"], "hbm_frac_per_rank": round(rr["hbm_GBps_per_rank"] / HBM_PEAK_GBS, 4),
+                    **{k: v for k, v in sc.items() if k not in ("what", "ms_per_step")}}
         optional(res, "tp_llama2_7b" if c4_head else "tp", tp_rccl, ctx)
     if tp > 1:
         res["tp"] = tp_summary(r)
@@ -1270,7 +1325,9 @@ def main():
             def c4_tp():
                 c4 = CONFIGS["llama2-70b-m1"]
                 rc = measure_tp(ctx, c4, merge, world, max(2, a.steps // 2), max(1, a.warmup // 2))
-                return {
+                ms1 = measure_alone(ctx, c4, merge, max(2, a.steps // 2), max(1, a.warmup // 2))
+                sc = scaling_vs_1gpu(rc["ms_per_step"], ms1, world, "")
+                return {**{k: v for k, v in sc.items() if k not in ("what", "ms_per_step")},
                     "what": f"BASELINE config C4: {c4[3]}, column-parallel over {world} GPUs + one RCCL "
                             f"all-gather per linear ({c4[0]} layers, {len(launch_list(c4[2], merge))} launches each)",
                     "value": round(rc["flops_step"] / (rc["ms_per_step"] / 1e3) / 1e12, 4),
@@ -1291,6 +1348,7 @@ def main():
         if res.get("c4_llama2_70b_1gpu", {}).get("value"):
             res["c4_llama2_70b_1gpu"]["note"] = ("C4's one-GPU point: bench.py --gpus N (N > 1) reports C4 split "
                                                  "over the N GPUs as `value`")
+            res["c4_llama2_70b_1gpu"]["baseline_for"] = "--gpus N --parallel c4 (the N > 1 default): value"
     if not a.no_layers and not prefill and a.config.startswith("llama2-7b"):
         optional(res, "decoder_layers_e2e", lambda: {
             "what": f"LLaMA-2-7B decoder layers end to end (32 layers; RMSNorm, qkv, o, gate_up, SiLU*up, down, "

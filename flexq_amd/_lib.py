@@ -64,7 +64,7 @@ _SIGS = {
     "fq_chain_workspace_init": ([P, SZ, P], I),
     "fq_chain_error_offset": ([], SZ),
     "fq_chain_workspace_bytes": ([P, I, I], SZ),
-    "fq_chain_bind_status": ([P, P, P], I),
+    "fq_chain_bind_status": ([P, SZ, P, P], I),
     "fq_chain_status": ([P], I),
     "fq_chain_reset": ([P, SZ, P], I),
     "fq_ref_bit_packing": ([P, P, I, I, I, P], I),

@@ -30,15 +30,20 @@ struct Scratch {
 // Library-owned device memory of the instances: never freed while the process runs (a captured
 // graph bakes these addresses in), superseded buffers retired instead.
 std::mutex g_mu;
-// an imported weight image, the stream its import was enqueued on, an event recorded behind an eager
-// import (null once it has completed), and whether the import was captured into a graph (it then runs
-// only when the graph replays: no other stream may use the image)
+// an imported weight image, the stream its import was enqueued on, and an event recorded behind the
+// import (null once it has completed).  Imports are always eager: an import captured into a graph would
+// fill the image only when that graph replays, so an eager exec (or another graph) before the replay
+// would read it unfilled -- the first exec of a weight inside a capture is refused.
 struct Image {
     void *img;
     hipStream_t owner;
     hipEvent_t ready;
-    bool captured;
 };
+
+bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return !(hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone);
+}
 std::map<WeightKey, Image> g_images;
 std::map<hipStream_t, Scratch> g_scratch;
 std::vector<void *> g_retired;
@@ -80,14 +85,8 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
     if (it != g_images.end()) {
         // another stream's first use must not overtake the import enqueued on the owner's stream
         Image &im = it->second;
-        if (s != im.owner && im.captured) {  // filled by a graph replay only: nothing orders another stream
-            report(FQ_ERR_HIP, "FQBMMA exec: weight image imported inside a graph capture, used from another stream "
-                               "(run the first exec eagerly, or only on the capturing stream)");
-            return nullptr;
-        }
         if (im.ready && s != im.owner) {
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+            const bool capturing = stream_capturing(s);
             if (hipEventQuery(im.ready) == hipSuccess) {
                 (void)hipEventDestroy(im.ready);
                 im.ready = nullptr;  // the import has completed: no stream needs to wait any more
@@ -104,6 +103,11 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
         }
         return im.img;
     }
+    if (stream_capturing(s)) {
+        report(FQ_ERR_HIP, "FQBMMA exec: first use of a weight inside a graph capture (run the first exec eagerly: "
+                           "its import would only run when the graph replays)");
+        return nullptr;
+    }
     void *img = nullptr;
     const size_t bytes = fq_packed_w_bytes(a.N, a.K);
     if (hipMalloc(&img, bytes) != hipSuccess) {
@@ -117,14 +121,11 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
         return nullptr;
     }
     hipEvent_t ready = nullptr;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const bool captured = !(hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone);
-    if (!captured && hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess &&
-        hipEventRecord(ready, s) != hipSuccess) {
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess && hipEventRecord(ready, s) != hipSuccess) {
         (void)hipEventDestroy(ready);
         ready = nullptr;
     }
-    g_images[key] = Image{img, s, ready, captured};
+    g_images[key] = Image{img, s, ready};
     g_device_bytes += bytes;
     return img;
 }
@@ -132,6 +133,10 @@ const void *weight_image(const FQBMMAOpState::Argument_t &a, hipStream_t s) {
 void *stream_scratch(size_t need, hipStream_t s, size_t *bytes) {
     std::lock_guard<std::mutex> lk(g_mu);
     Scratch &sc = g_scratch[s];
+    if (sc.bytes < need && stream_capturing(s)) {  // (its zeroing would run only when the graph replays)
+        report(FQ_ERR_HIP, "FQBMMA exec: scratch growth inside a graph capture (run the shape eagerly first)");
+        return nullptr;
+    }
     if (sc.bytes < need) {
         // geometric growth (x1.5, 1 MiB granules): a rising sequence of shapes allocates O(log) times
         size_t nb = sc.bytes + sc.bytes / 2;

@@ -387,6 +387,32 @@ __device__ __forceinline__ void dequant4(float (&c)[4], v4i acc, __half2 p01, __
 #ifndef FQ_CHAIN_AHEAD
 #define FQ_CHAIN_AHEAD 1
 #endif
+// The ring prologue's placement and order, shared by decode_body and chain_ring_ahead (which issues a
+// chain linear's first ring blocks from the previous linear's tail, and must put exactly those blocks in
+// exactly the slots decode_body then reads): the wave's LDS region, its staged w-scales
+// after the D ring slots, the first block's byte offset in the image and the jump from an item's last
+// group to the next item's first.
+struct RingGeom {
+    char *ring;      // slot i at ring + i * SLOT
+    char *ws_st;     // staged w-scales: 32 B per block of the wave's sequence
+    uint32_t roff;   // byte offset of the wave's first block (item tile t0, group ga)
+    uint32_t rjump;  // an item's last group -> the next item's first (tiles tstep apart)
+};
+template <int MT, int XS, int SS>
+__device__ __forceinline__ RingGeom ring_geom(char *smem, int wid, int ngmax, int IPW, int M, int xwin, int pro, int t0,
+                                              int tstep, int G, int ga, int ng) {
+    using C = DecodeCfg<MT, XS, SS>;
+    RingGeom r;
+    r.ring = smem + wid * decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, xwin, decode_pro_windows(pro));
+    r.ws_st = r.ring + C::D * C::SLOT;
+    r.roff = ((uint32_t)t0 * G + ga) * FQ_BLOCK;
+    r.rjump = ((uint32_t)tstep * G - ng + 1) * FQ_BLOCK;
+    return r;
+}
+// the w-scales of the wave's block b (item b / ng, group ga + b % ng): 16 fp16 = 32 B, lanes 2b', 2b' + 1
+__device__ __forceinline__ const uint16_t *ws_stage_src(const uint16_t *wsb, int tile, int G, int ga, int j, int lane) {
+    return wsb + ((long)tile * G + ga + j) * 16 + 8 * (lane & 1);
+}
 template <int MT>
 __device__ __forceinline__ void chain_ring_ahead(uint32_t nxt_w, uint32_t nxt_p) {
     using C = DecodeCfg<MT, 0, 0>;
@@ -408,14 +434,15 @@ __device__ __forceinline__ void chain_ring_ahead(uint32_t nxt_w, uint32_t nxt_p)
     const int nit = IPW - (ir != 0) + (bid < ir ? 1 : 0);
     const int ngmax = (G + NW - 1) / NW, ga = (wid * G) / NW, ng = ((wid + 1) * G) / NW - ga, n = ng * nit;
     if (n <= 0) return;
-    char *ring = smem + wid * decode_wave_lds(MT, 0, 0, ngmax, ngmax * IPW, M, xwin, decode_pro_windows(0));
-    char *ws_st = ring + D * C::SLOT;
+    // (decode_body's V2 fused plan at S = 1: t0 = the workgroup, tstep = the grid, PRO 0)
+    const RingGeom rg = ring_geom<MT, 0, 0>(smem, wid, ngmax, IPW, M, xwin, 0, bid, grid, G, ga, ng);
+    char *ring = rg.ring, *ws_st = rg.ws_st;
     const uint32_t *wpk = reinterpret_cast<const uint32_t *>(wa);
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, (int)((uint32_t)NT * G * FQ_BLOCK), 0x00020000);
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
-    const uint32_t wvo = lane * 16, rjump = ((uint32_t)grid * G - ng + 1) * FQ_BLOCK;
-    uint32_t roff = ((uint32_t)bid * G + ga) * FQ_BLOCK;
+    const uint32_t wvo = lane * 16, rjump = rg.rjump;
+    uint32_t roff = rg.roff;
     int rj = 0;
 #pragma unroll
     for (int i = 0; i < D; i++) {
@@ -433,7 +460,7 @@ __device__ __forceinline__ void chain_ring_ahead(uint32_t nxt_w, uint32_t nxt_p)
         if (i == 0) {  // the w-scales, 32 blocks (32 B = 2 lanes each) per instruction (decode_body's stage_all)
             for (int i0 = 0; i0 < n; i0 += 32) {
                 const int b = i0 + (lane >> 1) < n ? i0 + (lane >> 1) : n - 1;
-                __builtin_amdgcn_global_load_lds(wsb + ((long)(bid + (b / ng) * grid) * G + ga + b % ng) * 16 + 8 * (lane & 1),
+                __builtin_amdgcn_global_load_lds(ws_stage_src(wsb, bid + (b / ng) * grid, G, ga, b % ng, lane),
                                                  LDS_PTR(ws_st + i0 * 32), 16, 0, 0);
             }
         }
@@ -504,9 +531,10 @@ __device__ __forceinline__ void decode_body(
     // blocked w-scales of the image: fp16 [NT][G][16] after the weight blocks (fq_quant.hip)
     const uint16_t *wsb = reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(wpk) + (size_t)NT * G * FQ_BLOCK);
 
+    const RingGeom rgeo = ring_geom<MT, XS, SS>(smem, wid, ngmax, IPW, M, FUSE ? xwin : 0, PRO, t0, tstep, G, ga, ng);
     const int wl = decode_wave_lds(MT, XS, SS, ngmax, ngmax * IPW, M, FUSE ? xwin : 0, decode_pro_windows(PRO));
-    char *ring = smem + wid * wl;
-    char *ws_st = ring + D * C::SLOT;                                 // staged w-scales
+    char *ring = rgeo.ring;
+    char *ws_st = rgeo.ws_st;                                         // staged w-scales
     char *xs_st = ws_st + (SS ? 0 : decode_wsst_bytes(ngmax * IPW));  // staged x-scales
     char *x_st = xs_st + (SS ? 0 : decode_xsst_bytes(ngmax, MT));     // staged activations
     const int EM = M * 16;                                            // live elements of a tile
@@ -665,7 +693,7 @@ __device__ __forceinline__ void decode_body(
         if (n > 0 && !SS && !(ABL & 8)) {
             for (int i0 = 0; i0 < n; i0 += 32) {  // w-scales: 32 blocks (32 B = 2 lanes each) per instruction
                 const int i = i0 + (lane >> 1) < n ? i0 + (lane >> 1) : n - 1;
-                __builtin_amdgcn_global_load_lds(wsb + ((long)item_tile(i / ng) * G + ga + i % ng) * 16 + 8 * (lane & 1),
+                __builtin_amdgcn_global_load_lds(ws_stage_src(wsb, item_tile(i / ng), G, ga, i % ng, lane),
                                                  LDS_PTR(ws_st + i0 * 32), 16, 0, 0);
             }
             if (!FUSE) {
@@ -708,8 +736,8 @@ __device__ __forceinline__ void decode_body(
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, (int)((uint32_t)NT * G * FQ_BLOCK), 0x00020000);
     const uint32_t wvo = lane * 16;
-    uint32_t roff = ((uint32_t)t0 * G + ga) * FQ_BLOCK;                 // next block to issue
-    const uint32_t rjump = ((uint32_t)tstep * G - ng + 1) * FQ_BLOCK;  // an item's last group -> the next item's first
+    uint32_t roff = rgeo.roff;          // next block to issue
+    const uint32_t rjump = rgeo.rjump;  // an item's last group -> the next item's first
     // Every DMA of the ring and the staging goes through a buffer resource with a per-lane offset fixed
     // for the launch and the block / group in an SGPR offset (never the instruction's immediate: on an
     // LDS-DMA it moves the LDS destination too), so the unfused variants' refills carry no 64-bit
@@ -829,6 +857,12 @@ __device__ __forceinline__ void decode_body(
     const bool eupd = CHN && pro.link == 1 && blockIdx.x == 0 && wid == 0 && chain_late(pro.epoch) != 0xfffffffeu;
     const uint32_t eseen = eupd ? chain_epoch_load(pro.chain) : 0u;
 
+    // A chain wave whose wait failed -- it timed out, or the workspace's error word was set (another
+    // workgroup timed out, in this launch or an earlier one) -- makes every output of its workgroup for
+    // this linear fp16 NaN (its partials are NaN, so the reduction's sums are), so a caller that never
+    // reads the status word cannot consume the undefined results silently.  Later
+    // linears of the launch see the error word as they start and fail at once.
+    bool cfail = false;
     if (CHN && !CHP && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers; from the hand-off,
         // each lane's four granules re-loaded until every tag is this launch's tag
         const uint32_t want = gr ? chain_tag(chain_late(pro.epoch)) : 0u;
@@ -849,8 +883,11 @@ __device__ __forceinline__ void decode_body(
             } else {
                 for (int spin = 0; spin < (1 << 20); spin++) {
                     // every granule load of the pass in flight at once, then the tag compares (a
-                    // short-circuit && between them serialises one round trip per load pair)
+                    // short-circuit && between them serialises one round trip per load pair); a re-poll
+                    // also loads the error word in the same round trip (the first pass does not: it
+                    // is the common case, and the word was read as the linear started)
                     uint4 g0[4], g1[4];
+                    const uint32_t ew = spin ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         if (c + 4 * u < R) {
@@ -858,6 +895,7 @@ __device__ __forceinline__ void decode_body(
                             g1[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u] + 16, 0, 16));
                         }
                     }
+                    failed = failed || ew != 0u;
                     bool ok = true;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
@@ -883,6 +921,7 @@ __device__ __forceinline__ void decode_body(
                 x_store(c + 4 * u + (lane >> 4), codes, sh);
             }
         }
+        cfail = failed;
         FQ_CSTAMP(2);
     } else if (CHP && n > 0) {  // ---- the chain with producer links (a separate instantiation): two sources
         // each lane's four granules re-loaded until every tag is this launch's tag
@@ -898,8 +937,9 @@ __device__ __forceinline__ void decode_body(
             bool dx = !gr, din = !gin;
             for (int spin = 0; spin < (1 << 20); spin++) {
                 // every load of the pass in flight at once, then the tag compares (a short-circuit &&
-                // between them serialises one round trip per load pair)
+                // between them serialises one round trip per load pair); a re-poll loads the error word too
                 uint4 gx0[4], gx1[4], gi0[4], gi1[4];
+                const uint32_t ew = spin ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     if (c + 4 * u < R) {
@@ -935,6 +975,7 @@ __device__ __forceinline__ void decode_body(
                 }
                 dx = dx || __builtin_amdgcn_ballot_w64(!okx) == 0;  // (wave-uniform)
                 din = din || __builtin_amdgcn_ballot_w64(!okin) == 0;
+                failed = failed || ew != 0u;
                 if ((dx && din) || failed) break;
                 __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
                 if (spin == (1 << 20) - 1) {
@@ -943,12 +984,14 @@ __device__ __forceinline__ void decode_body(
                 }
             }
             FQ_CSTAMP(6);
+            cfail = failed;
             if (CHP && cpro == 1) {  // residual add + RMSNorm (M = 1, K = 4 x 128 x NW: lane = chunk 64 wid + lane,
                                   // as the fused producer kernel, PRO 1 above -- the same bits)
                 uint4 r = v[0];
                 const uint4 gg = gg0;
                 if (hasin) {
                     r = add_residual8(w[0], r);
+                    if (failed) r = make_uint4(0x7e007e00u, 0x7e007e00u, 0x7e007e00u, 0x7e007e00u);  // (NaN residual)
                     if (blockIdx.x == 0) {
                         *reinterpret_cast<uint4 *>(pro.res_out + chn_el(0, 0)) = r;
                         if (pro.hr) {  // the residual for a later linear of the chain: four granules
@@ -1211,6 +1254,12 @@ __device__ __forceinline__ void decode_body(
             continue;
         }
         const int rs = it % RC;
+        if (CHN && cfail) {  // (wave-uniform; the chain's failed wait: NaN partials)
+#pragma unroll
+            for (int rg = 0; rg < RG; rg++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) cur[rg][r] = __builtin_nanf("");
+        }
 #pragma unroll
         for (int rg = 0; rg < RG; rg++)
 #pragma unroll
@@ -2794,6 +2843,7 @@ static fq_status chain_bind(void *chain_ws, uint32_t *host_status, hipStream_t s
         (void)hipGetLastError();  // (not device-mapped memory: clear the sticky error)
         return FQ_ERR_NULL;
     }
+    *(volatile uint32_t *)host_status = 0u;  // (a word that starts nonzero would read as a timeout)
     hipLaunchKernelGGL(fq_chain_bind_kernel, dim3(1), dim3(64), 0, s, (uint32_t *)chain_ws, (uint64_t)(uintptr_t)dev);
     FQ_LAUNCH_CHECK();
     std::lock_guard<std::mutex> lk(g_chain_mu);
@@ -2801,9 +2851,11 @@ static fq_status chain_bind(void *chain_ws, uint32_t *host_status, hipStream_t s
     return FQ_OK;
 }
 
-extern "C" fq_status fq_chain_bind_status(void *chain_ws, uint32_t *host_status, fq_stream_t stream) {
+extern "C" fq_status fq_chain_bind_status(void *chain_ws, size_t chain_ws_bytes, uint32_t *host_status,
+                                          fq_stream_t stream) {
     if (!chain_ws || !host_status) return FQ_ERR_NULL;
-    if ((uintptr_t)chain_ws & 255) return FQ_ERR_WORKSPACE;
+    // (the bind kernel writes the word's address at byte 32 * 4 * FQ_CHAIN_HOST of the sync area)
+    if (((uintptr_t)chain_ws & 255) || chain_ws_bytes < FQ_CHAIN_SYNC_BYTES) return FQ_ERR_WORKSPACE;
     return chain_bind(chain_ws, host_status, (hipStream_t)stream);
 }
 

@@ -79,7 +79,9 @@ def workspace(device, nbytes, stream_handle):
 
 
 _CWS = {}  # (device, stream) -> chain workspace (fq_chain_workspace_init; written by chain launches only)
-_CWS_STATUS = {}  # id(chain workspace) -> its pinned host status word (fq_chain_bind_status), kept for the process
+_CWS_STATUS = {}  # chain workspace data_ptr -> its pinned host status word (fq_chain_bind_status)
+_CWS_HOSTS = []  # every host status word ever bound, kept for the process: a superseded workspace may still
+                 # have a chain in flight whose timed-out wait stores into its word
 
 
 def chain_workspace(device, nbytes, stream_handle):
@@ -98,8 +100,10 @@ def chain_workspace(device, nbytes, stream_handle):
         _lib.call("fq_chain_workspace_init", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(stream_handle))
         if hasattr(_lib.load(), "fq_chain_bind_status"):  # (an older A/B build may lack it)
             host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            _lib.call("fq_chain_bind_status", _ptr(buf), ctypes.c_void_p(host.data_ptr()), ctypes.c_void_p(stream_handle))
-            _CWS_STATUS[id(buf)] = host
+            _lib.call("fq_chain_bind_status", _ptr(buf), ctypes.c_size_t(nbytes), ctypes.c_void_p(host.data_ptr()),
+                      ctypes.c_void_p(stream_handle))
+            _CWS_STATUS[buf.data_ptr()] = host
+            _CWS_HOSTS.append(host)
         _CWS[key] = buf
     if torch.cuda.is_current_stream_capturing():
         _WS_CAPTURED.add(id(buf))

@@ -138,9 +138,21 @@ class FLEXQGEMMWrapper {
         return true;
     }
 
+    static bool capturing(hipStream_t stream) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        return !(hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone);
+    }
+
+    /* an import (or a scratch zeroing) enqueued inside a graph capture would run only when the graph
+     * replays, so an eager call before that would read an unfilled image: the first use of a weight
+     * and scratch growth are refused while the stream captures (make the first call eagerly) */
     const void *image_for(const int *B, const uint16_t *w_scale, int N, int K, hipStream_t stream) {
         auto it = images_.find(B);
         if (it != images_.end()) return it->second.ptr;
+        if (capturing(stream)) {
+            report(FQ_ERR_HIP, "first use of a weight inside a graph capture (make the first call eagerly)");
+            return nullptr;
+        }
         void *img = nullptr;
         if (hipMalloc(&img, fq_packed_w_bytes(N, K)) != hipSuccess) {
             report(FQ_ERR_HIP, "weight image allocation");
@@ -170,6 +182,8 @@ class FLEXQGEMMWrapper {
     bool scratch(int M, int N, int K, hipStream_t stream, Scratch *out) {
         const size_t wsr = ws_region(M, N, K);
         const size_t need = wsr + align((size_t)M * K) + align((size_t)M * (K / 128) * 2);
+        if (need > scratch_bytes_ && capturing(stream))
+            return report(FQ_ERR_HIP, "scratch growth inside a graph capture (make the first call of this shape eagerly)");
         if (need > scratch_bytes_) {
             size_t nb = scratch_bytes_ + scratch_bytes_ / 2;  // geometric growth
             if (nb < need) nb = need;

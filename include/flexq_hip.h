@@ -49,7 +49,9 @@ typedef struct ihipStream_t *fq_stream_t; /* == hipStream_t */
  * fq_bmma_init_image) and fq_bmma_state carries w_format / prepared; split-K prefill without its
  * workspace returns FQ_ERR_WORKSPACE.  A caller built against another version should compare
  * FQ_ABI_VERSION with fq_abi_version() at start-up. */
-#define FQ_ABI_VERSION 4   /* 4: FQ_ERR_TIMEOUT and the host-visible chain status (fq_chain_bind_status) */
+#define FQ_ABI_VERSION 5   /* 4: FQ_ERR_TIMEOUT and the host-visible chain status (fq_chain_bind_status);
+                              5: fq_chain_bind_status takes the chain workspace's size and zeroes the word,
+                                 a timed-out chain writes NaN outputs */
 int fq_abi_version(void);
 
 typedef int fq_status;
@@ -145,7 +147,9 @@ fq_status fq_linear_w6ax(const uint16_t *x, int M, int N, int K, int abits, cons
  * written by chain launches only (one per stream; it may serve every chain of that stream).
  * A chain launch never hangs: a wait that does not end within ~1 s sets the word at byte offset
  * fq_chain_error_offset() of chain_ws (sticky; results undefined; every later wait on that workspace
- * returns at once) and, when a host status word is bound (fq_chain_bind_status), that word too; from
+ * returns at once) and, when a host status word is bound (fq_chain_bind_status), that word too; every
+ * output of a linear whose wait failed (or saw the error word) is written as fp16 NaN, so the undefined
+ * results cannot be consumed silently by a caller that does not read the status; from
  * then on fq_linear_chain_w6ax on chain_ws returns FQ_ERR_TIMEOUT without enqueuing anything, until
  * fq_chain_reset (the reference's convention: FQBMMAOp::initialize sets initSuccess = false and the
  * wrapper prints and returns, flexq_bmma_op.h:103-126, flexq_gemm_wrapper.cu:93).
@@ -175,11 +179,13 @@ fq_status fq_linear_chain_w6ax(const fq_chain_link *links, int n, int M, void *c
 size_t fq_chain_workspace_bytes(const fq_chain_link *links, int n, int M);
 fq_status fq_chain_workspace_init(void *chain_ws, size_t bytes, fq_stream_t stream);
 size_t fq_chain_error_offset(void);
-/* Host-visible chain status.  host_status (host): a zeroed 4-byte word of pinned, device-mapped host
- * memory (hipHostMalloc, or torch's pinned memory), owned by the caller and kept alive with chain_ws.
- * Binding enqueues one small kernel on `stream` that records the word's device address in chain_ws
- * (call it after fq_chain_workspace_init).  FQ_ERR_NULL when host_status is not device-mapped. */
-fq_status fq_chain_bind_status(void *chain_ws, uint32_t *host_status, fq_stream_t stream);
+/* Host-visible chain status.  host_status (host): a 4-byte word of pinned, device-mapped host memory
+ * (hipHostMalloc, or torch's pinned memory), owned by the caller and kept alive with chain_ws (and while
+ * any launch on chain_ws may be in flight).  Binding zeroes the word (on the host) and enqueues one small
+ * kernel on `stream` that records its device address in chain_ws (call it after fq_chain_workspace_init).
+ * FQ_ERR_NULL when host_status is not device-mapped; FQ_ERR_WORKSPACE when chain_ws is not 256-byte
+ * aligned or chain_ws_bytes is below the chain's sync area (4096 bytes; the word's address lives there). */
+fq_status fq_chain_bind_status(void *chain_ws, size_t chain_ws_bytes, uint32_t *host_status, fq_stream_t stream);
 /* FQ_ERR_TIMEOUT once a wait on chain_ws timed out (the bound word, read on the host: no
  * synchronisation, so a timeout shows once the launch that hit it has finished); FQ_OK otherwise,
  * also for a workspace without a bound word.  A captured graph's replays do not pass through

@@ -14,6 +14,8 @@
  *   fqo_gemm               the contract: int32 per-group accumulators (exact) dequantised with the
  *                          fp16-rounded scale product of flexq_bmma_kernel.h:360-364, summed in
  *                          double and rounded once to fp16.
+ *   fqo_gemm_decode_order  the decode kernel's own fp32 summation order (S = 1): a bit-exact model of
+ *                          the headline kernel's output, not a reference function.
  *   fqo_pack_fq6 / fqo_unpack_fq6   this build's own 6-bit weight image --
  *                          a model of the HIP packer, not a reference function.
  *   fqo_rmsnorm_quantize   e2e/src/fastertransformer/kernels/layernorm_kernels.cu:1851-2051
@@ -269,6 +271,39 @@ int fqo_gemm(const int8_t *xq, const uint16_t *xs, const int8_t *wq, const uint1
             }
             out[(size_t)m * N + n] = f64_to_f16(sum);
             if (mag_out) mag_out[(size_t)m * N + n] = mag;
+        }
+    return 0;
+}
+
+/* The decode kernel's own fp32 summation order -- a bit-exact model of the production decode / chain
+ * output for plans without a k-split (flexq_amd/csrc/fq_gemm.hip decode_body, S = 1; every LLaMA decode
+ * shape at M = 1 and every chain link), so the headline's fp16 outputs can be checked bit for bit rather
+ * than within a tolerance.  Not a reference function: the reference's own order (compute_ref,
+ * fqo_compute_ref) differs in the last bits.  Per output (m, n): wave w of NW owns groups
+ * [w*G/NW, (w+1)*G/NW) and accumulates c = fmaf(float(4 * acc_g), float(half(xs * ws)), c) from 0 in
+ * group order (the MFMA sums 4*w, fq_common.h unpack_fq6); the workgroup sums the NW partials c * 0.25 in
+ * wave order from 0 and rounds once to fp16. */
+int fqo_gemm_decode_order(const int8_t *xq, const uint16_t *xs, const int8_t *wq, const uint16_t *ws, int M, int N,
+                          int K, int NW, uint16_t *out) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 128 != 0 || NW <= 0) return 1;
+    const int G = K / 128;
+    for (int m = 0; m < M; m++)
+        for (int n = 0; n < N; n++) {
+            float v = 0.0f;
+            for (int w = 0; w < NW; w++) {
+                float c = 0.0f;
+                for (int g = (w * G) / NW; g < ((w + 1) * G) / NW; g++) {
+                    const int8_t *xr = xq + (size_t)m * K + (size_t)g * 128;
+                    const int8_t *wr = wq + (size_t)n * K + (size_t)g * 128;
+                    int32_t a = 0;
+                    for (int i = 0; i < 128; i++) a += (int32_t)xr[i] * (int32_t)wr[i];
+                    const float p = f16_to_f32(fqo_f32_to_f16(f16_to_f32(xs[(size_t)g * M + m]) *
+                                                              f16_to_f32(ws[(size_t)g * N + n])));
+                    c = fmaf((float)(4 * a), p, c);
+                }
+                v = v + c * 0.25f;
+            }
+            out[(size_t)m * N + n] = fqo_f32_to_f16(v);
         }
     return 0;
 }

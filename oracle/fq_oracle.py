@@ -41,6 +41,7 @@ def lib():
             "fqo_quantize_engine": [P, I, I, I, P, P],
             "fqo_compute_ref": [P, P, P, P, P, I, I, I, I, I],
             "fqo_gemm": [P, P, P, P, I, I, I, P, P, P],
+            "fqo_gemm_decode_order": [P, P, P, P, I, I, I, I, P],
             "fqo_xs_to_ref_dup": [P, I, I, P],
             "fqo_pack_fq6": [P, P, I, I, P],
             "fqo_unpack_fq6": [P, I, I, P, P],
@@ -180,6 +181,21 @@ def gemm(xq, xs, wq, ws, want_acc=False):
     _check(lib().fqo_gemm(_p(xq), _p(xs), _p(wq), _p(ws), M, N, K, _p(out),
                           _p(acc) if want_acc else None, _p(mag)), "gemm")
     return out, acc, mag
+
+
+def gemm_decode_order(xq, xs, wq, ws, nw=8):
+    """The decode kernel's exact fp32 summation order at S = 1 (NW waves per workgroup: 8 for M <= 16)
+    -> D fp16 [M,N], bit-identical to the production decode / chain output (fq_oracle.c)."""
+    xq = np.ascontiguousarray(xq, dtype=np.int8)
+    wq = np.ascontiguousarray(wq, dtype=np.int8)
+    xs = np.ascontiguousarray(xs, dtype=np.float16)
+    ws = np.ascontiguousarray(ws, dtype=np.float16)
+    M, K = xq.shape
+    N = wq.shape[0]
+    out = np.zeros((M, N), dtype=np.float16)
+    f = lib().fqo_gemm_decode_order
+    _check(f(_p(xq), _p(xs), _p(wq), _p(ws), M, N, K, int(nw), _p(out)), "gemm_decode_order")
+    return out
 
 
 def check_div_by_const(hi):

@@ -119,3 +119,39 @@ def test_chain_runs_cut_at_the_attention_cores():
     assert [r[1] for r in runs[1]] == ["wo0", "wgate_up0", "wdown0", "wqkv1"]
     assert [r[1] for r in runs[-1]] == ["wo31", "wgate_up31", "wdown31"]
     assert sum(len(r) for r in runs) == 128
+
+
+def test_multi_gpu_line_is_like_for_like():
+    """an N > 1 line carries the same workload's one-GPU point measured in the same run
+    (same_workload_1gpu: ms per step, speedup, strong-scaling efficiency), the 7B split's and C4's own
+    one-GPU points, and the world size / backend the collectives ran on -- and keeps them, under the
+    driver's 6,000-character limit, on a synthetic N = 8 result padded with every optional section."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, "profiles", "r05_final_share2_rehearsal.json")) as f:
+        res = json.loads(f.readline())
+    res.pop("rehearsal", None)
+    res["n_gpus"] = 8
+    res["comm"] = {"world_size": 8, "backend": "nccl", "rccl_version": "2.26.6"}
+    res["same_workload_1gpu"] = bench.scaling_vs_1gpu(1.60, 8.83, 8, "C4 unsharded on one GPU vs its split")
+    res["tp_llama2_7b"].update({k: v for k, v in bench.scaling_vs_1gpu(0.70, 1.16, 8, "").items()
+                                if k not in ("what", "ms_per_step")})
+    res["c4_llama2_70b_tp"] = dict(res["tp"], **{k: v for k, v in bench.scaling_vs_1gpu(1.6, 8.83, 8, "").items()
+                                                 if k not in ("what", "ms_per_step")})
+    big = _r04_result()  # the N = 1 sections, as if a run had them all
+    for k in ("vs_reference_sweep", "vs_rocblas_fp16", "c3_llama2_7b_m16", "c5_llama3_8b_prefill"):
+        res[k] = big[k]
+    line = bench.compact_line(res, "gpurun_out/bench_detail.json")
+    text = json.dumps(line)
+    assert len(text) <= bench.LINE_MAX, len(text)
+    sw = line["same_workload_1gpu"]
+    assert sw["ms_per_step_1gpu"] == 8.83 and sw["speedup_vs_1gpu"] == round(8.83 / 1.60, 4)
+    assert sw["strong_scaling_efficiency"] == round(8.83 / 1.60 / 8, 4)
+    assert line["comm"] == {"world_size": 8, "backend": "nccl", "rccl_version": "2.26.6"}
+    assert line["vs_baseline"] is None  # BASELINE.md publishes no number for this metric
+    for k in bench.ESSENTIAL:
+        assert k in line or k == "cpu_baseline", k  # (the CPU baseline is timed at N = 1 only)
+    # last resort (a line that would not fit even without the optional sections) keeps them too
+    tiny = bench.compact_line(res, None, limit=10)
+    assert "same_workload_1gpu" in tiny and "comm" in tiny

@@ -181,16 +181,35 @@ def test_chain_error_word_fails_fast_and_recovers(ops, dev):
     words[9 * 32] = 1
     t0 = time.time()
     for _ in range(3):
+        for (*_, out) in links:
+            out.zero_()
         ops.linear_chain_w6ax(links)
     torch.cuda.synchronize()
     assert time.time() - t0 < 5.0
     assert ops.chain_error(dev) == 1
+    assert_failed_outputs_nan(ops, links, dev, "error word set")
     words[9 * 32] = 0
     for (*_, out) in links:
         out.fill_(float("nan"))
     ops.linear_chain_w6ax(links)
     torch.cuda.synchronize()
     check(ops, links, dev, "after clearing the error word")
+
+
+def assert_failed_outputs_nan(ops, links, dev, what):
+    """After a failed chain launch: every link that waited for a previous link's
+    output wrote fp16 NaN over its whole output; a run's first link (its input ready before the launch)
+    waited for nothing and holds its right bits."""
+    ref = sequential(ops, links, dev)
+    for i, ((x, _, _, _, out), r) in enumerate(zip(links, ref)):
+        prev = links[i - 1][4] if i else None
+        waited = prev is not None and prev.data_ptr() <= x.data_ptr() < prev.data_ptr() + prev.numel() * 2
+        o = out.cpu()
+        if waited:
+            assert bool(torch.isnan(o).all()), f"{what}: link {i} has {int((~torch.isnan(o)).sum())} non-NaN outputs"
+        else:
+            np.testing.assert_array_equal(o.numpy().view(np.uint16), r.cpu().numpy().view(np.uint16),
+                                          err_msg=f"{what}: link {i} (ready input)")
 
 
 def test_headline_step_pinned_to_the_oracle(ops, dev):
@@ -200,7 +219,8 @@ def test_headline_step_pinned_to_the_oracle(ops, dev):
     oracle is bit-identical to the engine's codes and scales; the oracle's int32 group accumulators over the
     link's weight image (unpacked by the oracle) equal the debug kernel's bit for bit
     (engine/test_bgemm_kernel.cu:113-146's check); the chain's fp16 output equals that debug launch's bit for
-    bit and lies within oracle.gemm_tolerance of the oracle's."""
+    bit, lies within oracle.gemm_tolerance of the oracle's, and equals bit for bit the oracle's restatement
+    of the decode kernel's own fp32 summation order (oracle.gemm_decode_order)."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -227,6 +247,11 @@ def test_headline_step_pinned_to_the_oracle(ops, dev):
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), d_dbg.cpu().numpy().view(np.uint16),
                                       err_msg=f"link {i}: chain output vs the debug launch")
         assert_gemm_close(out.cpu().numpy(), ref, mag, f"headline link {i} ({N}x{K})")
+        # and directly: the chain's own fp16 output bit for bit against the oracle's restatement of the
+        # decode kernel's fp32 summation order (8 waves, S = 1)
+        exact = oracle.gemm_decode_order(q, s, wq, ws, nw=8)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), exact.view(np.uint16),
+                                      err_msg=f"link {i}: chain output vs the oracle's decode-order sum")
 
 
 def test_chain_host_status_raises_until_reset(ops, dev):
@@ -239,7 +264,7 @@ def test_chain_host_status_raises_until_reset(ops, dev):
     torch.cuda.synchronize()
     assert not ops.chain_status(dev)
     buf = ops.chain_workspace_buffer(dev)
-    ops._CWS_STATUS[id(buf)][0] = 1  # as chain_fail's system-scope store would
+    ops._CWS_STATUS[buf.data_ptr()][0] = 1  # as chain_fail's system-scope store would
     with pytest.raises(_lib.ChainTimeoutError):
         ops.linear_chain_w6ax(links)
     ops.chain_reset(dev)
@@ -254,8 +279,9 @@ def test_chain_host_status_raises_until_reset(ops, dev):
 def test_chain_not_coresident_times_out_and_recovers(ops, dev):
     """The co-residency failure: a kernel on another stream holds half of the CUs for 2.5 s
     while a chain launches, so half of the chain's workgroups cannot start.  The resident ones' waits end
-    after ~1 s with the error word set (never a hang); the kernel itself writes the bound host word, the
-    next call raises ChainTimeoutError, and after chain_reset the chain is bit-exact again."""
+    after ~1 s with the error word set (never a hang); the kernel itself writes the bound host word and NaN
+    over every output that depended on the failed waits, the next call raises ChainTimeoutError, and after
+    chain_reset the chain is bit-exact again."""
     import ctypes
     import os
     import time
@@ -268,6 +294,8 @@ def test_chain_not_coresident_times_out_and_recovers(ops, dev):
     links = build(ops, dev, 1, LAYER_7B * 2, seed=14)
     ops.linear_chain_w6ax(links)  # the workspace exists and is bound
     torch.cuda.synchronize()
+    for (*_, out) in links:
+        out.zero_()
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     sink = torch.zeros(cus, dtype=torch.int32, device=dev)
     side = torch.cuda.Stream(dev)
@@ -280,6 +308,7 @@ def test_chain_not_coresident_times_out_and_recovers(ops, dev):
     assert time.time() - t0 < 30.0
     assert ops.chain_error(dev) == 1, "the chain could not have been co-resident"
     assert ops.chain_status(dev), "the kernel did not write the bound host status word"
+    assert_failed_outputs_nan(ops, links, dev, "co-residency timeout")
     with pytest.raises(_lib.ChainTimeoutError):
         ops.linear_chain_w6ax(links)
     ops.chain_reset(dev)

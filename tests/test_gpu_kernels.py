@@ -691,6 +691,77 @@ def test_gemm_prefill_sampled(ops, dev, M, N, K, abits, with_acc):
                       f"prefill M={M} N={N} K={K}")
 
 
+# C5 (LLaMA-3-8B prefill, M = 16384, W6A8) through the PRODUCTION 256 x 256 kernel (no debug output:
+# the fp16 result of the launch the bench times) on every C5 width, against the oracle on a sample
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("N,K", [(6144, 4096), (28672, 4096), (4096, 14336)])
+def test_c5_production_kernel_sampled(ops, dev, N, K):
+    M = 16384
+    g = torch.Generator(device=dev).manual_seed(N + K)
+    xq_d = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq_d = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs_d = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws_d = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq_d, ws_d)
+    w_u8 = ops.prepare_prefill_weights(pk, N, K)
+    d = ops.gemm_w6ax(xq_d, xs_d, pk, N, 8, w_u8=w_u8)
+    r = rng(N + 7 * K)
+    rows = np.sort(np.concatenate([r.choice(M, size=62, replace=False), [0, M - 1]]))
+    cols = np.sort(np.concatenate([r.choice(N, size=94, replace=False), [0, N - 1]]))
+    rows_t, cols_t = torch.from_numpy(rows).to(dev), torch.from_numpy(cols).to(dev)
+    ref, _, mag = oracle.gemm(host(xq_d.index_select(0, rows_t)), np.ascontiguousarray(host(xs_d.index_select(1, rows_t))),
+                              host(wq_d.index_select(0, cols_t)), np.ascontiguousarray(host(ws_d.index_select(1, cols_t))))
+    assert_gemm_close(host(d.index_select(0, rows_t).index_select(1, cols_t)), ref, mag, f"C5 production {N}x{K}")
+
+
+@pytest.mark.timeout(300)
+def test_c5_epilogue_quantized_codes_against_the_oracle(ops, dev):
+    """C5's gate_up -> down hand-off as the bench runs it (fq_gemm_w6ax_u8_q: the next linear's A8 codes and
+    scales from the 256 x 256 GEMM's epilogue; the next input [16384, 14336] is the output's leading
+    values, rows straddling output rows): sampled rows of the codes and scales bit-exact against the
+    oracle's engine quantizer applied to the GEMM's own fp16 output, and that output within the oracle's
+    GEMM tolerance."""
+    M, N, K, qM, qK = 16384, 28672, 4096, 16384, 14336
+    g = torch.Generator(device=dev).manual_seed(31)
+    xq = torch.randint(-128, 128, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    w_u8 = ops.prepare_prefill_weights(pk, N, K)
+    d, qxq, qxs = ops.gemm_w6ax_q(xq, xs, pk, N, 8, w_u8, (qM, qK), 8)
+    torch.cuda.synchronize()
+    r = rng(11)
+    qrows = np.sort(np.concatenate([r.choice(qM, size=30, replace=False), [0, qM - 1]]))
+    qr_t = torch.from_numpy(qrows).to(dev)
+    x_next = d.view(-1)[:qM * qK].view(qM, qK).index_select(0, qr_t)
+    q_ref, s_ref = oracle.quantize_engine(host(x_next), 8)
+    np.testing.assert_array_equal(host(qxq.index_select(0, qr_t)), q_ref)
+    np.testing.assert_array_equal(host(qxs.index_select(1, qr_t)).view(np.uint16), s_ref.view(np.uint16))
+    rows = np.sort(np.concatenate([r.choice(M, size=30, replace=False), [0, M - 1]]))
+    cols = np.sort(np.concatenate([r.choice(N, size=62, replace=False), [0, N - 1]]))
+    rows_t, cols_t = torch.from_numpy(rows).to(dev), torch.from_numpy(cols).to(dev)
+    ref, _, mag = oracle.gemm(host(xq.index_select(0, rows_t)), np.ascontiguousarray(host(xs.index_select(1, rows_t))),
+                              host(wq.index_select(0, cols_t)), np.ascontiguousarray(host(ws.index_select(1, cols_t))))
+    assert_gemm_close(host(d.index_select(0, rows_t).index_select(1, cols_t)), ref, mag, "C5 gate_up (epilogue form)")
+
+
+# M = 1 decode linears of the headline workload (every plan S = 1): the fused one-launch output bit for
+# bit against the oracle's restatement of the decode kernel's summation order
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 4096), (22016, 4096), (4096, 11008)])
+def test_decode_linear_bit_exact_decode_order(ops, dev, N, K):
+    g = torch.Generator(device=dev).manual_seed(N ^ K)
+    x = torch.randn((1, K), dtype=torch.float16, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    ws = ((torch.rand((K // 128, N), device=dev, generator=g) + 0.5) / (18.5 * K ** 0.5)).half()
+    pk = ops.pack_w6(wq, ws)
+    y = ops.linear_w6ax(x, pk, N, 6)
+    torch.cuda.synchronize()
+    q, s = oracle.quantize_engine(host(x), 6)
+    exact = oracle.gemm_decode_order(q, s, host(wq), host(ws), nw=8)
+    np.testing.assert_array_equal(host(y).view(np.uint16), exact.view(np.uint16))
+
+
 @pytest.mark.timeout(300)
 def test_quantize_act_past_4g_elements(ops, dev):
     """fq_quantize_act over M x K > 2^32 elements (its 64-bit index form): sampled rows bit-exact

@@ -11,10 +11,23 @@
 #   shapes   graph-timed decode launches (tools/shape_sweep.py; SHAPES="N K ...", M=..., FQ_SWEEP=...)
 #   prefill  prefill GEMMs (tools/prefill_bench.py at PF_M, default 16384)
 # Libraries are selected with FLEXQ_AMD_LIB / FQ_LIB (flexq_amd/_lib.py); build variants with
-#   make -C flexq_amd/csrc variant NAME=x DEFS="-DFOO=1"   ->  tools/libflexq_hip_x.so
+#   make -C flexq_amd/csrc variant NAME=x DEFS="-DFOO=1"   ->  abtmp/libflexq_hip_x.so
+# (abtmp/ is git-ignored; clear it after the experiment so later pushes do not carry the libraries)
+# AB_TESTS="tests/test_gpu_chain.py ..."  runs those GPU tests against EVERY library first and stops on a
+#   failure (an A/B of a variant that is not bit-identical is not an A/B); AB_OUT=file tees the table.
+# One gpurun call per experiment:  AB_TESTS=... bash tools/ab.sh step 3 flexq_amd/libflexq_hip.so abtmp/x.so
 set -o pipefail
 MODE=$1; REPS=$2; shift 2
-[ -n "$MODE" ] && [ -n "$REPS" ] && [ $# -ge 1 ] || { sed -n 2,16p "$0"; exit 2; }
+[ -n "$MODE" ] && [ -n "$REPS" ] && [ $# -ge 1 ] || { sed -n 2,20p "$0"; exit 2; }
+mkdir -p gpurun_out
+if [ -n "$AB_TESTS" ]; then
+  for L in "$@"; do
+    FLEXQ_AMD_LIB=$L timeout -k 10 600 python3 -u -m pytest $AB_TESTS -x -q --timeout 200 --timeout-method thread \
+      > gpurun_out/ab_tests.log 2>&1 || { echo "tests failed with $L"; tail -30 gpurun_out/ab_tests.log; exit 1; }
+    echo "$L: $(tail -1 gpurun_out/ab_tests.log)"
+  done
+fi
+[ -n "$AB_OUT" ] && exec > >(tee "$AB_OUT")
 B="python3 -u bench.py --cpu-budget 0 --no-fp16-compare --no-calibrate"
 J='import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1])'
 for rep in $(seq "$REPS"); do

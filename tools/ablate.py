@@ -1,4 +1,4 @@
-"""Decode-GEMM ablation timing (development tool; needs tools/libflexq_hip_abl.so built with
+"""Decode-GEMM ablation timing (development tool; needs abtmp/libflexq_hip_abl.so built with
 -DFQ_DEV_ABLATION).  For each ablation mask, captures a HIP graph of R GEMM launches per shape
 (weights rotated over several copies so the MALL cannot hold them) and prints us/launch.
   mask 2: no MFMA/dequant   4: no cross-wave reduction/fix-up   6: both (pure streaming)
@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "abtmp", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [(12288, 4096), (4096, 4096), (11008, 4096), (4096, 11008), (28672, 8192), (8192, 28672)]

@@ -1,4 +1,4 @@
-"""Decode-chain timeline (development tool; tools/libflexq_hip_abl.so).  Runs the bench's layer
+"""Decode-chain timeline (development tool; abtmp/libflexq_hip_abl.so).  Runs the bench's layer
 chain (o -> gate_up -> down -> qkv, LLaMA-2-7B, M = 1, each input the leading K values of the previous
 output) in a graph, then reads the per-(WG, linear) wave-0 stamps (s_memrealtime, 100 MHz): 0 linear
 start, 1 ring issued (a linear after the first: its prologue; the ring itself went out from the
@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "abtmp", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [("o", 4096, 4096, 6), ("gate_up", 22016, 4096, 6), ("down", 4096, 11008, 6), ("qkv", 12288, 4096, 6)]

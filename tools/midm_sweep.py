@@ -1,4 +1,4 @@
-"""32 < M <= 256 (development tool, tools/libflexq_hip_abl.so): the decode kernel in row chunks of
+"""32 < M <= 256 (development tool, abtmp/libflexq_hip_abl.so): the decode kernel in row chunks of
 32 (FQ_DEV_MIDM=1) against the 128 x 128 prefill kernel with split-K (FQ_DEV_MIDM=0).  Per shape:
 int32 group accumulators identical and outputs within 1e-3 relative between the two paths, then
 graph-timed GEMM launches (24 per graph over rotating weight copies, as tools/shape_sweep.py).
@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("FQ_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+_lib.LIB_PATH = os.environ.get("FQ_LIB", os.path.join(ROOT, "abtmp", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [(4096, 4096), (12288, 4096), (22016, 4096), (4096, 11008)]

@@ -1,5 +1,5 @@
 """Where a group step of the 256 x 256 prefill kernel spends its cycles (development tool;
-tools/libflexq_hip_abl.so, FQ_DEV_ABLATION = 128 + 32).  Per wave of the first 256 workgroups,
+abtmp/libflexq_hip_abl.so, FQ_DEV_ABLATION = 128 + 32).  Per wave of the first 256 workgroups,
 s_memtime sums of four segments of every group step: the barrier wait, the stage DMA issue (waves
 4-7 issue it all), the compute (LDS reads, MFMAs, dequant) and the trailing wait for the next
 stage.  Prints cycles per group step by wave, averaged over the workgroups.  The stamps fence the
@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "abtmp", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 

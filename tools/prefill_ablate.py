@@ -1,4 +1,4 @@
-"""Prefill GEMM ablations (development tool; needs tools/libflexq_hip_abl.so, `make -C
+"""Prefill GEMM ablations (development tool; needs abtmp/libflexq_hip_abl.so, `make -C
 flexq_amd/csrc abl`).  FQ_DEV_ABLATION bits: 1 no dequant, 2 no MFMA, 4 no LDS reads,
 8 no global loads / DMA, 16 no stores, 32 no A DMA, 64 no weight loads.  M >= 2048: the U8 path
 (weights unpacked once per call) like the product.
@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "abtmp", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 

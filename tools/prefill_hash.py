@@ -1,7 +1,7 @@
 """Hash of the prefill GEMM outputs (development tool: bit-identity of variant libraries, FQ_LIB).
 Prints one sha256 per shape of fq_gemm_w6ax's fp16 output on seeded inputs (the 256 x 256 path and
 a ragged one).
-usage: FQ_LIB=tools/libflexq_hip_x.so python tools/prefill_hash.py"""
+usage: FQ_LIB=abtmp/libflexq_hip_x.so python tools/prefill_hash.py"""
 import hashlib
 import os
 import sys

@@ -1,4 +1,4 @@
-"""Decode-kernel timeline (development tool; tools/libflexq_hip_abl.so, ablation mask 16).
+"""Decode-kernel timeline (development tool; abtmp/libflexq_hip_abl.so, ablation mask 16).
 Per workgroup s_memrealtime stamps (100 MHz): 0 entry, 1 ring prologue issued, 2 first block
 landed, 3 item loop done, 4 split-K fix-up done.  Prints, per shape, the kernel span against the
 graph-replay time per launch, the dispatch skew and the phase medians (us).  FQ_STAMP_M: rows (default
@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from flexq_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "tools", "libflexq_hip_abl.so"))
+_lib.LIB_PATH = os.environ.get("FQ_ABL_LIB", os.path.join(ROOT, "abtmp", "libflexq_hip_abl.so"))
 from flexq_amd import ops  # noqa: E402
 
 SHAPES = [(12288, 4096), (4096, 4096), (11008, 4096), (4096, 11008), (28672, 8192), (8192, 28672)]
