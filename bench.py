@@ -881,7 +881,7 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
     Returns ms per token step for both and, with several ranks, the W6 step without its
     all-reduces."""
     from flexq_amd import convert
-    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear, run_layers, run_layers_chained
+    from flexq_amd.layers import FlexQDecoderLayer, FlexQFfn, W6Linear, run_layers
     dev, tp, rank = ctx.dev, ctx.world, ctx.rank
     g = torch.Generator(device=dev).manual_seed(seed)  # the same full weights on every rank
     sq, sf = H ** -0.5, F ** -0.5
@@ -920,9 +920,6 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
         if pending is not None:
             torch.add(cur, pending, out=h)
 
-    def step_w6_chain(h):  # the same layers as decode chains (one launch per layer at M = 1; one rank)
-        run_layers_chained(w6, h)
-
     def step_16(h):
         F_ = torch.nn.functional
         for W in w16:
@@ -941,34 +938,19 @@ def decoder_layers_e2e(ctx, M, layers=32, H=4096, F=11008, reps=5, seed=77):
     h0 = torch.randn((M, H), dtype=torch.float16, device=dev, generator=g)
     hs = {k: h0.clone() for k in ("w6", "w6_noreduce", "fp16")}
     fns = {"w6": lambda: step_w6(hs["w6"]), "fp16": lambda: step_16(hs["fp16"])}
-    if tp == 1 and M <= 4:
-        hs["w6_chain"] = h0.clone()
-        fns["w6_chain"] = lambda: step_w6_chain(hs["w6_chain"])
     if tp > 1:
         fns["w6_noreduce"] = lambda: step_w6_noreduce(hs["w6_noreduce"])
-    finals = {}
     for name, fn in fns.items():
         replay = ctx.prepare(fn, not ctx.a.no_graph and not ctx.staged)
         hs[name].copy_(h0)
-        replay()  # one step from h0: the outputs compared below
+        replay()
         torch.cuda.synchronize()
-        finals[name] = hs[name].clone()
         el, _ = ctx.timed(replay, reps, 2)
         out[name] = el / reps * 1e3
         hs[name].copy_(h0)
-    if "w6_chain" in out:  # the chain form: bit-identical one-step output to the launches' required
-        same = bool(torch.equal(finals["w6_chain"].view(torch.int16), finals["w6"].view(torch.int16)))
-        err = ops.chain_error(dev, stream=ctx.stream)
-        chain = {"w6_chain_ms_per_step": round(out["w6_chain"], 4), "bit_identical_to_launches": same,
-                 "wait_timed_out": bool(err), "launches_ms_per_step": round(out["w6"], 4)}
-        if same and not err and out["w6_chain"] < out["w6"]:
-            out["w6"] = out["w6_chain"]
-            chain["taken"] = True
     res = {"w6_ms_per_step": round(out["w6"], 4), "fp16_ms_per_step": round(out["fp16"], 4),
            "speedup_vs_fp16": round(out["fp16"] / out["w6"], 3), "tok_per_s": round(M * 1e3 / out["w6"], 2),
            "fp16_tok_per_s": round(M * 1e3 / out["fp16"], 2)}
-    if "w6_chain" in out:
-        res["decode_chain"] = chain
     if tp > 1:
         res["w6_no_allreduce_ms_per_step"] = round(out["w6_noreduce"], 4)
         res["allreduce_share"] = round(max(0.0, 1 - out["w6_noreduce"] / out["w6"]), 4)

@@ -69,8 +69,11 @@ __host__ __device__ constexpr int decode_waves(int MT) { return MT <= 16 ? FQ_DE
 #ifndef FQ_RING_DMAX
 #define FQ_RING_DMAX 3
 #endif
+// (64-row tiles, activations per slot: three slots of a block + 64 activation rows + their scales,
+// so the weight stream keeps three blocks per wave in flight as the small-M kernels do)
 __host__ __device__ constexpr int decode_ring_budget(int MT, int XS) {
-    return (decode_waves(MT) == 8 ? FQ_RING_BUDGET : 2 * FQ_RING_BUDGET) / (XS == 0 && MT > 4 ? 2 : 1);
+    return MT >= 64 && XS ? 3 * (FQ_BLOCK + 8 * 1024 + 64 + 64 * 4)
+                          : (decode_waves(MT) == 8 ? FQ_RING_BUDGET : 2 * FQ_RING_BUDGET) / (XS == 0 && MT > 4 ? 2 : 1);
 }
 __host__ __device__ constexpr int decode_depth_cap(int U) { return 63 / U + 1 < FQ_RING_DMAX ? 63 / U + 1 : FQ_RING_DMAX; }
 __host__ __device__ constexpr int decode_depth_for(int MT, int XS, int slot, int U) {
@@ -84,7 +87,7 @@ __host__ __device__ constexpr int decode_depth_for(int MT, int XS, int slot, int
 // SS: w-/x-scales staged (0) or carried per ring slot (1).
 // XSR: x-scale record per group in LDS (dwords; rows >= M are read but never used).
 template <int MT, int XS, int SS> struct DecodeCfg {
-    static constexpr int RG = MT <= 16 ? 1 : 2;                  // 16-row MFMA row groups
+    static constexpr int RG = MT <= 16 ? 1 : MT / 16;            // 16-row MFMA row groups
     static constexpr int XSR = 16 * RG;
     static constexpr int XP = XS ? (MT <= 8 ? 1 : MT / 8) : 0;  // 1 KiB activation pieces per slot
     static constexpr int WS_OFF = FQ_BLOCK + XP * 1024;         // slot scales (SS = 1)
@@ -214,10 +217,13 @@ __device__ __forceinline__ void gather_poll(const fq_gather *__restrict__ g, uin
 // epoch word every workgroup reads as the launch starts (a run's hand-off buffers are disjoint), so
 // no granule an earlier launch left matches.  Every workgroup adds 1 to its shard of a start counter
 // after reading E; workgroup 0, in linear 1's prologue, waits until all have (they have long since),
-// then stores E + 1 and zeroes the shards for the next launch.  The launch whose tag is 2^32 - 1 ends
+// then stores E + 1 and zeroes the shards for the next launch.  The launch whose tag is 2^31 - 1 ends
 // with a fan-in whose last workgroup zeroes the hand-off region and the epoch (tags never repeat
-// over a granule's lifetime).  Bounded: a wait that does not end within ~1 s sets the error word and
-// goes on (results undefined, never a hang); with the error word set later waits return at once.
+// over a granule's lifetime, and never have bit 31 set).  Bounded: a wait that does not end within
+// ~1 s sets the error word and goes on; with the error word set later waits return at once.  A linear
+// whose wait failed writes fp16 NaN outputs and tags its granules with bit 31 set (poisoned): its
+// consumers stop waiting on them and fail in turn, so every output downstream of a failure is NaN
+// (results are never undefined-but-plausible) at no cost to the normal path.
 constexpr int FQ_CHAIN_MAX = 8;
 constexpr size_t FQ_CHAIN_SYNC_BYTES = 4096;       // chain workspace: sync words, then the hand-offs
 constexpr int FQ_CHAIN_EPOCH = 8, FQ_CHAIN_ERR = 9, FQ_CHAIN_DONE = 10;  // sync words, 128 B apart;
@@ -232,6 +238,9 @@ __device__ __forceinline__ void chain_fail(uint32_t *__restrict__ sync) {
     const uint64_t h = __hip_atomic_load(reinterpret_cast<uint64_t *>(sync + 32 * FQ_CHAIN_HOST), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     if (h) __hip_atomic_store(reinterpret_cast<uint32_t *>(h), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // (the failure path retires its own loads: otherwise a load left pending on this rare path makes the
+    // compiler wait vmcnt(0) -- the next linear's whole ring -- at the chain's link loop head)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 // The epoch is loaded as the launch starts and first needed a linear later: every use goes through
 // this (volatile: not hoisted to the load), so no wave waits for it before its first DMA.
@@ -854,7 +863,7 @@ __device__ __forceinline__ void decode_body(
         if (n > 0) x_fetch(0);
     }
     // workgroup 0 advances the epoch around linear 1 (not in the launch whose tag wraps)
-    const bool eupd = CHN && pro.link == 1 && blockIdx.x == 0 && wid == 0 && chain_late(pro.epoch) != 0xfffffffeu;
+    const bool eupd = CHN && pro.link == 1 && blockIdx.x == 0 && wid == 0 && chain_late(pro.epoch) != 0x7ffffffeu;
     const uint32_t eseen = eupd ? chain_epoch_load(pro.chain) : 0u;
 
     // A chain wave whose wait failed -- it timed out, or the workspace's error word was set (another
@@ -863,6 +872,9 @@ __device__ __forceinline__ void decode_body(
     // reads the status word cannot consume the undefined results silently.  Later
     // linears of the launch see the error word as they start and fail at once.
     bool cfail = false;
+#ifndef FQ_CHAIN_NAN
+#define FQ_CHAIN_NAN 1  // (development: 0 = the round-5 chain without the NaN outputs, A/B builds)
+#endif
     if (CHN && !CHP && n > 0) {  // ---- the chain: activations by sc1 buffer loads to registers; from the hand-off,
         // each lane's four granules re-loaded until every tag is this launch's tag
         const uint32_t want = gr ? chain_tag(chain_late(pro.epoch)) : 0u;
@@ -883,11 +895,8 @@ __device__ __forceinline__ void decode_body(
             } else {
                 for (int spin = 0; spin < (1 << 20); spin++) {
                     // every granule load of the pass in flight at once, then the tag compares (a
-                    // short-circuit && between them serialises one round trip per load pair); a re-poll
-                    // also loads the error word in the same round trip (the first pass does not: it
-                    // is the common case, and the word was read as the linear started)
+                    // short-circuit && between them serialises one round trip per load pair)
                     uint4 g0[4], g1[4];
-                    const uint32_t ew = spin ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         if (c + 4 * u < R) {
@@ -895,7 +904,6 @@ __device__ __forceinline__ void decode_body(
                             g1[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off[u] + 16, 0, 16));
                         }
                     }
-                    failed = failed || ew != 0u;
                     bool ok = true;
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
@@ -937,9 +945,8 @@ __device__ __forceinline__ void decode_body(
             bool dx = !gr, din = !gin;
             for (int spin = 0; spin < (1 << 20); spin++) {
                 // every load of the pass in flight at once, then the tag compares (a short-circuit &&
-                // between them serialises one round trip per load pair); a re-poll loads the error word too
+                // between them serialises one round trip per load pair); poisoned tags as the plain chain's
                 uint4 gx0[4], gx1[4], gi0[4], gi1[4];
-                const uint32_t ew = spin ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     if (c + 4 * u < R) {
@@ -975,7 +982,6 @@ __device__ __forceinline__ void decode_body(
                 }
                 dx = dx || __builtin_amdgcn_ballot_w64(!okx) == 0;  // (wave-uniform)
                 din = din || __builtin_amdgcn_ballot_w64(!okin) == 0;
-                failed = failed || ew != 0u;
                 if ((dx && din) || failed) break;
                 __builtin_amdgcn_s_sleep(FQ_CHAIN_SLEEP);
                 if (spin == (1 << 20) - 1) {
@@ -1254,12 +1260,6 @@ __device__ __forceinline__ void decode_body(
             continue;
         }
         const int rs = it % RC;
-        if (CHN && cfail) {  // (wave-uniform; the chain's failed wait: NaN partials)
-#pragma unroll
-            for (int rg = 0; rg < RG; rg++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) cur[rg][r] = __builtin_nanf("");
-        }
 #pragma unroll
         for (int rg = 0; rg < RG; rg++)
 #pragma unroll
@@ -1267,6 +1267,19 @@ __device__ __forceinline__ void decode_body(
                 const int row = 16 * rg + 4 * (lane >> 4) + r;
                 if (row < M) red[(rs * NW + wid) * EM + row * 16 + (lane & 15)] = cur[rg][r] * 0.25f;
             }
+        // the chain's failed wait: NaN partials, overwritten in LDS (a branch that leaves cur alone: one that
+        // set cur to NaN changed the register allocation enough to add a vmcnt(0) -- the next linear's whole
+        // ring -- at the chain's link loop head, 1.7 % per step)
+        if (CHN && FQ_CHAIN_NAN && cfail) {  // (wave-uniform)
+            const uint32_t nan = 0x7fc00000u;
+#pragma unroll
+            for (int rg = 0; rg < RG; rg++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = 16 * rg + 4 * (lane >> 4) + r;
+                    if (row < M) ds_write_b32(lds_addr(red + (rs * NW + wid) * EM + row * 16 + (lane & 15)), nan);
+                }
+        }
         if (rs == RC - 1 || it == nit - 1) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
@@ -1443,7 +1456,7 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_ln_kerne
 // every granule (all the others are done reading), the start counter and the epoch.
 __device__ __forceinline__ void chain_wrap_end(uint32_t *__restrict__ sync, uint32_t epoch, uint4 *hand,
                                                uint32_t hand_bytes) {
-    if (chain_late(epoch) != 0xfffffffeu) return;
+    if (chain_late(epoch) != 0x7ffffffeu) return;
     __syncthreads();
     __shared__ uint32_t last;
     if (threadIdx.x == 0) {
@@ -2453,14 +2466,14 @@ static const int kSplitQuantCost4 = 12;
 static DecodePlan decode_plan(int M, int N, int K, bool fused, int pro = 0) {
     DecodePlan p;
     p.pro = fused ? pro : 0;
-    p.MT = M <= 4 ? 4 : (M <= 8 ? 8 : (M <= 16 ? 16 : 32));
+    p.MT = M <= 4 ? 4 : (M <= 8 ? 8 : (M <= 16 ? 16 : (M <= 32 ? 32 : 64)));
     const int NT = (N + 15) / 16, G = K / FQ_GROUP;
     p.NT = NT;
     p.NCH = 1;
     const int cus = device_cus();
     const int NW = decode_waves(p.MT);
-    if (M > 32) {  // row chunks of 32: every chunk streams the whole weight image, no k-split
-        p.NCH = (M + 31) / 32;
+    if (M > 32) {  // row chunks of 64: every chunk streams the whole weight image, no k-split
+        p.NCH = (M + 63) / 64;
         p.S = 1;
         p.xwin = 0;
         const int items = NT * p.NCH;
@@ -2585,14 +2598,17 @@ static int prefill_split(int M, int N, int K) {
 #endif
     return bs;
 }
-// 32 < M <= 64: the decode kernel in two row chunks of 32 (each chunk streams the weights, in one
-// launch) or the 128 x 128 prefill kernel (split-K when its tiles are few).  Measured
-// (tools/midm_sweep.py, M = 33 .. 256 on four LLaMA-2-7B shapes): the chunks win only while a chunk
-// is one round of tiles over short K -- 4096 x 4096 at M = 33 .. 64: 11.2-11.5 vs 14.3-16.5 us --
-// and lose from 12288 columns, K = 11008 or three chunks on (up to 2.5 x).
+// 32 < M <= 128: the decode kernel with 64-row tiles (each weight block streamed once for all 64 rows;
+// beyond 64 rows, row chunks of 64, each streaming the weights) or the 128 x 128 prefill kernel (split-K
+// when its tiles are few).  Measured (tools/midm_sweep.py, profiles/r06_midm_sweep.txt, us per GEMM launch,
+// decode / prefill): M = 33 .. 64 -- 4096 x 4096 8.9-9.3 / 13.6-15.7, 12288 x 4096 18.7-21.2 / 21.9-23.6,
+// 4096 x 11008 16.7-18.6 / 21.7-23.2, but 22016 x 4096 33.6-40.4 / 32.6-34.1 (5.4 tiles per CU: the
+// activation rows re-staged per tile); M = 96 .. 128 (two chunks) only 4096 x 4096 wins, 15.5 / 18.3-20.5.
+// (The round-5 rule, row chunks of 32, won only on 4096 x 4096: 11.2-11.5 us.)
 static bool midm_decode(int M, int N, int K) {
-    if (M <= 32 || M > 256) return false;
-    bool use = M <= 64 && (N + 15) / 16 <= device_cus() && K <= 4096;
+    if (M <= 32 || M > 128) return false;
+    const int NT = (N + 15) / 16;
+    bool use = M <= 64 ? NT <= 3 * device_cus() : (NT <= device_cus() && K <= 4096);
 #ifdef FQ_DEV_ABLATION
     if (const char *e = getenv("FQ_DEV_MIDM")) use = atoi(e) != 0;  // development: force either
 #endif
@@ -2719,11 +2735,15 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
 
 template <int MT, bool FUSE, bool DBG>
 static fq_status dispatch_modes(const DecodePlan &p, const DecodeArgs &a, hipStream_t stream) {
-    if (FUSE) return launch_decode<MT, 0, 0, true, DBG>(p, a, stream);
-    if (MT == 32 && p.NCH > 1) {  // row chunks
-        if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG, true>(p, a, stream);
-        if (p.SS == 0) return launch_decode<MT, 1, 0, false, DBG, true>(p, a, stream);
-        return launch_decode<MT, 1, 1, false, DBG, true>(p, a, stream);
+    if constexpr (MT == 64) {  // 32 < M: never fused; row chunks of 64 beyond 64 rows
+        if (FUSE) return FQ_ERR_SHAPE;
+        if (p.NCH > 1) {
+            if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG, true>(p, a, stream);
+            if (p.SS == 0) return launch_decode<MT, 1, 0, false, DBG, true>(p, a, stream);
+            return launch_decode<MT, 1, 1, false, DBG, true>(p, a, stream);
+        }
+    } else {
+        if (FUSE) return launch_decode<MT, 0, 0, true, DBG>(p, a, stream);
     }
     if (p.XS == 0) return launch_decode<MT, 0, 0, false, DBG>(p, a, stream);
     if (p.SS == 0) return launch_decode<MT, 1, 0, false, DBG>(p, a, stream);
@@ -2737,7 +2757,8 @@ static fq_status dispatch_decode(const DecodePlan &p, const DecodeArgs &a, hipSt
         case 4: return dispatch_modes<4, FUSE, DBG>(p, a, stream);
         case 8: return dispatch_modes<8, FUSE, DBG>(p, a, stream);
         case 16: return dispatch_modes<16, FUSE, DBG>(p, a, stream);
-        default: return dispatch_modes<32, FUSE, DBG>(p, a, stream);
+        case 32: return dispatch_modes<32, FUSE, DBG>(p, a, stream);
+        default: return dispatch_modes<64, FUSE, DBG>(p, a, stream);
     }
 }
 

@@ -140,7 +140,7 @@ __host__ __device__ inline int xswz(int row, int chunk) { return (chunk ^ (row &
 
 // ---- decode weight-image block and staged-region sizes (fq_gemm.hip, fq_seq.hip) ----
 constexpr int FQ_BLOCK = 1536;  // bytes of one (16-column tile, group) fq6 block
-__host__ __device__ inline int decode_xsr(int MT) { return MT <= 16 ? 16 : 32; }
+__host__ __device__ inline int decode_xsr(int MT) { return MT <= 16 ? 16 : MT; }
 // staged regions, rounded up to whole DMA instructions (each writes 64 lanes' worth)
 __host__ __device__ inline int decode_wsst_bytes(int nb) { return ((nb + 31) / 32) * 1024; }
 __host__ __device__ inline int decode_xsst_bytes(int ng, int MT) { return ((ng * decode_xsr(MT) + 63) / 64) * 256; }

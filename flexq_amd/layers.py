@@ -187,6 +187,10 @@ def run_layers_chained(layers, h, check=False):
     before the chain (as the bench's stand-in ctx = v does): a chain cannot run a kernel between its
     links.  The residual rotates through three buffers (h and two scratch), since a chain reads one and
     writes two.  Returns h.
+    Speed: measured SLOWER than run_layers' one-launch-per-linear form (1.353 vs 1.320 ms per 32-layer
+    LLaMA-2-7B step at M = 1, round 5: each producer hand-off -- the RMSNorm's cross-wave sum, SiLU * up
+    polling two sources -- costs more than the kernel boundary it removes), so bench.py no longer times it
+    and run_layers stays the decoder path; kept as a tested, bit-identical API.
     Failure: a chain wait that timed out (e.g. other kernels holding CUs the chain needs, include/flexq_hip.h)
     leaves the stream's chain workspace in the timed-out state, and the next call raises
     _lib.ChainTimeoutError before launching anything (ops.chain_reset clears it).  check=True also

@@ -43,10 +43,11 @@ def test_library_loads_and_reports():
     assert lib.fq_packed_w_bytes(17, 128) == 2 * 1 * (1536 + 32)
     assert lib.fq_packed_w_bytes(16, 100) == 0  # K % 128
     assert lib.fq_gemm_workspace_bytes(1024, 28672, 4096) == 0  # prefill, many tiles: no split-K slabs
-    # few tiles (M = 96, N = 4096: 32 WGs): split-K slabs after the ticket region, fp32 [S][M][Npad]
-    ws = lib.fq_gemm_workspace_bytes(96, 4096, 4096)
-    assert ws > 256 * 1024 and (ws - 256 * 1024) % (96 * 4096 * 4) == 0
-    assert lib.fq_gemm_workspace_bytes(64, 4096, 4096) == 0  # two row chunks of the decode kernel
+    # few tiles (M = 200, N = 4096: 64 WGs): split-K slabs after the ticket region, fp32 [S][M][Npad]
+    ws = lib.fq_gemm_workspace_bytes(200, 4096, 4096)
+    assert ws > 256 * 1024 and (ws - 256 * 1024) % (200 * 4096 * 4) == 0
+    assert lib.fq_gemm_workspace_bytes(64, 4096, 4096) == 0  # the decode kernel's 64-row tile
+    assert lib.fq_gemm_workspace_bytes(96, 4096, 4096) == 0  # two row chunks of 64
 
 
 def test_null_and_shape_errors_are_status_codes():

@@ -144,7 +144,8 @@ def test_chain_rejections(ops, dev):
 
 def test_chain_sync_words_and_epoch_wrap(ops, dev):
     """After every chain launch the start counter is zero and the epoch has advanced by one; the
-    launch whose tag is 2^32 - 1 clears the hand-off granules and the epoch (tags never repeat)."""
+    launch whose tag is 2^31 - 1 clears the hand-off granules and the epoch (tags never repeat, never
+    carry the poison bit 31)."""
     links = build(ops, dev, 1, LAYER_7B, seed=8)
     ops.linear_chain_w6ax(links)
     torch.cuda.synchronize()
@@ -155,7 +156,7 @@ def test_chain_sync_words_and_epoch_wrap(ops, dev):
     ops.linear_chain_w6ax(links)
     torch.cuda.synchronize()
     assert int(words[8 * 32].item()) == e0 + 1
-    words[8 * 32] = -2  # the next launch's tag is 0xffffffff
+    words[8 * 32] = 0x7ffffffe  # the next launch's tag is 2^31 - 1 (bit 31 marks poisoned granules)
     for rep, want in ((0, 0), (1, 1), (2, 2)):
         for (*_, out) in links:
             out.fill_(float("nan"))

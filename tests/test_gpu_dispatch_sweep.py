@@ -18,6 +18,9 @@ pytestmark = pytest.mark.gpu
 CASES = [
     (1, 4096, 4096, 6), (31, 1000, 1280, 6), (32, 4096, 4096, 8), (33, 4096, 4096, 6), (33, 4104, 2048, 8),
     (64, 4096, 4096, 6), (65, 4096, 4096, 8), (64, 12288, 4096, 6), (96, 1000, 4096, 6), (127, 4096, 11008, 8),
+    # the 64-row decode tile (33 <= M <= 64): activation rows per ring slot, x-scales staged or per slot,
+    # several tiles per workgroup, ragged M
+    (48, 22016, 4096, 6), (64, 4096, 11008, 8), (40, 1000, 1280, 8), (57, 4104, 14336, 6),
     (200, 2048, 1280, 6), (257, 768, 2048, 8), (511, 4096, 4096, 6), (1023, 1004, 1280, 8), (2047, 512, 1024, 6),
     (2048, 4096, 1024, 8), (2049, 1000, 1280, 6), (3072, 6144, 512, 8), (4096, 28672, 256, 6),
 ]

@@ -14,7 +14,8 @@
 #   make -C flexq_amd/csrc variant NAME=x DEFS="-DFOO=1"   ->  abtmp/libflexq_hip_x.so
 # (abtmp/ is git-ignored; clear it after the experiment so later pushes do not carry the libraries)
 # AB_TESTS="tests/test_gpu_chain.py ..."  runs those GPU tests against EVERY library first and stops on a
-#   failure (an A/B of a variant that is not bit-identical is not an A/B); AB_OUT=file tees the table.
+#   failure (an A/B of a variant that is not bit-identical is not an A/B); AB_TESTS_K="expr" selects with
+#   pytest -k (leave out tests of the behaviour the variant changes); AB_OUT=file tees the table.
 # One gpurun call per experiment:  AB_TESTS=... bash tools/ab.sh step 3 flexq_amd/libflexq_hip.so abtmp/x.so
 set -o pipefail
 MODE=$1; REPS=$2; shift 2
@@ -22,7 +23,7 @@ MODE=$1; REPS=$2; shift 2
 mkdir -p gpurun_out
 if [ -n "$AB_TESTS" ]; then
   for L in "$@"; do
-    FLEXQ_AMD_LIB=$L timeout -k 10 600 python3 -u -m pytest $AB_TESTS -x -q --timeout 200 --timeout-method thread \
+    FLEXQ_AMD_LIB=$L timeout -k 10 600 python3 -u -m pytest $AB_TESTS ${AB_TESTS_K:+-k "$AB_TESTS_K"} -x -q --timeout 200 --timeout-method thread \
       > gpurun_out/ab_tests.log 2>&1 || { echo "tests failed with $L"; tail -30 gpurun_out/ab_tests.log; exit 1; }
     echo "$L: $(tail -1 gpurun_out/ab_tests.log)"
   done
