@@ -8,6 +8,7 @@
 //
 // usage: test_wrapper <outdir> <M> <N> <K> <abits> <seed>
 //        test_wrapper growth          (scratch growth over ascending M stays logarithmic)
+//        test_wrapper capture         (a weight's first use inside a graph capture is refused)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -85,8 +86,82 @@ static int growth() {
     return w.retired_count() <= 16 ? 0 : 11;
 }
 
+// a weight's FIRST use inside a graph capture is refused (its import would fill the image
+// only when the graph replays, so an eager call before that would read it unfilled), by the wrapper and
+// by the FQBMMA instances; after an eager first use, capturing works and the replay matches the eager D.
+static int capture() {
+    const int M = 1, N = 1024, K = 1024;
+    __half *dx, *dd, *dws, *dxs;
+    int32_t *dwp, *dxp;
+    CK(hipMalloc(&dx, (size_t)M * K * 2));
+    CK(hipMalloc(&dd, (size_t)M * N * 2));
+    CK(hipMalloc(&dws, (size_t)(K / 128) * N * 2));
+    CK(hipMalloc(&dxs, (size_t)(K / 128) * 8 * 2));
+    CK(hipMalloc(&dwp, (size_t)6 * N * (K / 32) * 4));
+    CK(hipMalloc(&dxp, (size_t)6 * 8 * (K / 32) * 4));
+    std::vector<__half> hx((size_t)M * K), hws((size_t)(K / 128) * N);
+    std::vector<int32_t> hwp((size_t)6 * N * (K / 32));
+    for (auto &v : hx) v = __float2half(uniform() - 0.5f);
+    for (auto &v : hws) v = __float2half(uniform() * 0.01f);
+    for (auto &v : hwp) v = (int32_t)next_u32();
+    CK(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dws, hws.data(), hws.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dwp, hwp.data(), hwp.size() * 4, hipMemcpyHostToDevice));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    const float *wsf = reinterpret_cast<const float *>(dws);
+    flexq_amd::FLEXQGEMMWrapper w(6, 6, true);
+    hipGraph_t g;
+    // 1. the wrapper: a first use inside the capture is refused, nothing is enqueued
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    w.gemm(M, N, K, dx, dwp, nullptr, dd, nullptr, wsf, nullptr, nullptr, false, nullptr, 0, s);
+    const fq_status refused = w.status();
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphDestroy(g));
+    if (refused == FQ_OK) return 20;
+    // 2. eager first use, then a captured call replays to the same bits
+    std::vector<uint16_t> d_eager((size_t)M * N), d_graph((size_t)M * N);
+    w.gemm(M, N, K, dx, dwp, nullptr, dd, nullptr, wsf, nullptr, nullptr, false, nullptr, 0, s);
+    if (w.status() != FQ_OK) return 21;
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(d_eager.data(), dd, d_eager.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemset(dd, 0, (size_t)M * N * 2));
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    w.gemm(M, N, K, dx, dwp, nullptr, dd, nullptr, wsf, nullptr, nullptr, false, nullptr, 0, s);
+    const fq_status captured = w.status();
+    CK(hipStreamEndCapture(s, &g));
+    if (captured != FQ_OK) return 22;
+    hipGraphExec_t ge;
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, s));
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(d_graph.data(), dd, d_graph.size() * 2, hipMemcpyDeviceToHost));
+    if (d_eager != d_graph) return 23;
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    // 3. the FQBMMA instance: its first exec of a weight inside a capture is refused too (D untouched)
+    CK(hipMemset(dd, 0, (size_t)M * N * 2));
+    FQBMMAInitFn_t init_fn;
+    FQBMMAExecFn_t exec_fn;
+    pick(6, M, &init_fn, &exec_fn);
+    FQBMMAOpState st = (*init_fn)(dxp, dwp, dxs, dws, M, N, K, dd, 128, false);
+    if (!st.initSuccess) return 24;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    (*exec_fn)(st, s);
+    CK(hipStreamEndCapture(s, &g));
+    size_t nodes = 0;
+    CK(hipGraphGetNodes(g, nullptr, &nodes));
+    CK(hipGraphDestroy(g));
+    if (nodes != 0) return 25;  // (refused before enqueuing anything)
+    CK(hipStreamDestroy(s));
+    for (void *p : {(void *)dx, (void *)dd, (void *)dws, (void *)dxs, (void *)dwp, (void *)dxp}) CK(hipFree(p));
+    printf("capture refusals ok\n");
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc == 2 && std::string(argv[1]) == "growth") return growth();
+    if (argc == 2 && std::string(argv[1]) == "capture") return capture();
     if (argc != 7) {
         fprintf(stderr, "usage: %s outdir M N K abits seed\n", argv[0]);
         return 2;

@@ -50,3 +50,12 @@ def test_cpp_wrapper_scratch_growth_is_logarithmic(dev):
     r = subprocess.run([BIN, "growth"], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "growth calls=" in r.stdout
+
+
+def test_cpp_first_weight_use_inside_capture_is_refused(dev):
+    """FLEXQGEMMWrapper and the FQBMMA instances refuse a weight's first use while the stream
+    captures (its import would only run at replay; an eager call before that read an unfilled image);
+    after an eager first use a captured call replays to the eager bits."""
+    r = subprocess.run([BIN, "capture"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capture refusals ok" in r.stdout and "[FlexQ][Error]" in r.stderr
