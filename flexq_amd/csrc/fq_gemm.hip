@@ -1134,6 +1134,10 @@ __device__ __forceinline__ void decode_body(
     int arow[RG];  // A-operand rows (rows >= M mirror row M-1, never stored)
 #pragma unroll
     for (int rg = 0; rg < RG; rg++) arow[rg] = 16 * rg + (lane & 15) < M ? 16 * rg + (lane & 15) : M - 1;
+    if (ABL & 4096) {  // (development: every lane reads activation row 0 -- the M = 1 LDS access pattern)
+#pragma unroll
+        for (int rg = 0; rg < RG; rg++) arow[rg] = 0;
+    }
     const int Npad = NT * 16;
     int i = 0;     // position in the wave's block sequence
     int rslot = 0;  // its ring slot (V2: counted, no i % D)
@@ -2691,6 +2695,7 @@ static fq_status launch_decode(const DecodePlan &p, const DecodeArgs &a, hipStre
     }
         FQ_ABL(2) FQ_ABL(4) FQ_ABL(6) FQ_ABL(8) FQ_ABL(14) FQ_ABL(16) FQ_ABL(48) FQ_ABL(112)
         FQ_ABL(256) FQ_ABL(512) FQ_ABL(1024) FQ_ABL(768) FQ_ABL(1536) FQ_ABL(1792) FQ_ABL(2048) FQ_ABL(2052)
+        FQ_ABL(4096)
 #undef FQ_ABL
     }
 #endif

@@ -808,7 +808,7 @@ def test_prefill_split_k_without_workspace_is_an_error(ops, dev):
     import ctypes
     from flexq_amd import _lib
     L = _lib.load()
-    M, N, K = 96, 4096, 4096
+    M, N, K = 200, 4096, 4096
     assert L.fq_gemm_workspace_bytes(M, N, K) > 256 * 1024  # the plan splits K
     xq = torch.zeros((M, K), dtype=torch.int8, device=dev)
     xs = torch.zeros((K // 128, M), dtype=torch.float16, device=dev)
