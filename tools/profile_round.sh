@@ -36,7 +36,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/m16
 python3 tools/trace_summary.py gpurun_out/prof/m16/run_kernel_trace.csv > $P/${R}_m16_kernel_trace_summary.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/pf -o run -- python3 tools/prefill_bench.py 16384 > gpurun_out/prof/pf.log 2>&1
 python3 tools/trace_summary.py gpurun_out/prof/pf/run_kernel_trace.csv > $P/${R}_prefill_kernel_trace_summary.txt
-cp gpurun_out/prof/pf.log $P/${R}_prefill_bench.txt
+cp gpurun_out/prof/pf.log $P/${R}_prefill_bench_under_rocprof.txt
 # 4. C5 (LLaMA-3-8B W6A8 prefill, M = 16384) bench under the kernel trace
 echo "[profile_round] 4. C5 (LLaMA-3-8B W6A8 prefill, M = 16384) bench under the" ; date
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/c5 -o run -- $B --config llama3-8b-prefill --steps 2 --warmup 1 --no-calibrate > gpurun_out/prof/c5.log 2>&1
