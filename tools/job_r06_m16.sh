@@ -9,3 +9,5 @@ for a in 0 4096 0 4096; do
   FQ_DEV_ABLATION=$a FQ_LIB=abtmp/libflexq_hip_abl.so FQ_SWEEP=gemm timeout -k 10 120 python3 -u tools/shape_sweep.py 16 4096 4096 12288 4096 22016 4096 2>&1 | grep us/launch || exit 1
 done > gpurun_out/r06_m16_lds_abl.txt
 cat gpurun_out/r06_m16_lds_abl.txt
+# run-to-run spread of the 32-layer decoder step (r05 1.295 / 1.320 ms at M = 1, r06 final 1.346)
+AB_OUT=gpurun_out/r06_e2e_spread.txt timeout -k 10 700 bash tools/ab.sh e2e 3 flexq_amd/libflexq_hip.so || exit 1
