@@ -184,10 +184,11 @@ def run_step(stack, M, world, group=None, gather=True, staged=False):
 
 
 def run_step_qo(stack, M):
-    """The prefill step with each linear's activation quantize moved into the previous GEMM's
-    epilogue (ops.gemm_w6ax_q, fq_gemm_w6ax_u8_q): the first input is quantized by its own launch,
-    every later one by the GEMM that produces it -- the same codes as run_step's separate quantize
-    launches (each linear's input is the leading M x K values of the previous output)."""
+    """The step with each linear's activation quantize moved into the previous GEMM's epilogue
+    (ops.gemm_w6ax_q: fq_gemm_w6ax_u8_q at prefill sizes, fq_gemm_w6ax_q's decode form at M <= 16): the
+    first input is quantized by its own launch, every later one by the GEMM that produces it -- the same
+    codes as run_step's separate quantize launches (each linear's input is the leading M x K values of
+    the previous output)."""
     lins_ = linears(stack)
     p0 = lins_[0][1]
     xq, xs = ops.quantize_act(p0["x"], p0["abits"])
@@ -195,10 +196,10 @@ def run_step_qo(stack, M):
         if i + 1 < len(lins_):
             nx = lins_[i + 1][1]
             assert nx["x"].data_ptr() == p["out"].data_ptr() and tuple(nx["x"].shape) == (M, nx["K"])
-            _, xq, xs = ops.gemm_w6ax_q(xq, xs, p["pk"], p["Nl"], p["abits"], p["w_u8"], (M, nx["K"]), nx["abits"],
-                                        out=p["out"])
+            _, xq, xs = ops.gemm_w6ax_q(xq, xs, p["pk"], p["Nl"], p["abits"], p.get("w_u8"), (M, nx["K"]),
+                                        nx["abits"], out=p["out"])
         else:
-            ops.gemm_w6ax(xq, xs, p["pk"], p["Nl"], p["abits"], out=p["out"], w_u8=p["w_u8"])
+            ops.gemm_w6ax(xq, xs, p["pk"], p["Nl"], p["abits"], out=p["out"], w_u8=p.get("w_u8"))
 
 
 def chain_runs(stack):
@@ -809,15 +810,15 @@ def measure_single(ctx, name, merge, steps, warmup):
             chain["taken"] = True
         del replay_c
     qo = None
-    if M >= ops.PREFILL_U8_MIN_M and not ctx.a.no_qo:  # quantize in the producer's epilogue (same codes)
+    if (M >= ops.PREFILL_U8_MIN_M or 4 < M <= 16) and not ctx.a.no_qo:  # quantize in the producer's epilogue
         last_out = linears(stack)[-1][1]["out"]
         ref = last_out.clone()
         replay_q = ctx.prepare(lambda: run_step_qo(stack, M), not ctx.a.no_graph)
         el_q, ev_q = ctx.timed(replay_q, steps, warmup)
         same = bool(torch.equal(last_out.view(torch.int16), ref.view(torch.int16)))
         del ref
-        qo = {"what": "each linear's activation quantize in the previous prefill GEMM's epilogue "
-                      "(fq_gemm_w6ax_u8_q; the step's first input quantized by its own launch)",
+        qo = {"what": "each linear's activation quantize in the previous GEMM's epilogue "
+                      "(fq_gemm_w6ax_u8_q / fq_gemm_w6ax_q; the step's first input quantized by its own launch)",
               "ms_per_step": round(el_q / steps * 1e3, 4),
               "separate_quantize_ms_per_step": round(elapsed / steps * 1e3, 4),
               "last_output_identical": same}
@@ -860,8 +861,10 @@ def measure_single(ctx, name, merge, steps, warmup):
         per_launch = ev_s / (steps * n_lin)
         fused = {(N, K): ops.act_scratch_bytes(M, N, K) == 0 for (_, N, K, _) in launch_lins}
         bytes_launch = layers * sum(alg_bytes(M, N, K, ab, fused[(N, K)]) for (_, N, K, ab) in launch_lins) / n_lin
+        qtaken = qo is not None and qo.get("taken", False)
         out["roofline"] = {"kernel": "fq_gemm_decode_kernel" + ("<FUSE>" if all(fused.values()) else
-                                                                 " + the separate quantize launch"),
+                                                                 " with the next input's quantizer in its epilogue"
+                                                                 if qtaken else " + the separate quantize launch"),
                            "bound": "hbm", "achieved": round(bytes_launch / per_launch / 1e9, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(bytes_launch / per_launch / 1e9 / HBM_PEAK_GBS, 4),

@@ -83,6 +83,8 @@ _SIGS = {
     "fq_prefill_unpack_weights": ([P, I, I, P, P], I),
     "fq_gemm_w6ax_u8": ([P, P, P, P, I, I, I, I, P, P, P, SZ, P], I),
     "fq_gemm_w6ax_u8_q": ([P, P, P, P, I, I, I, I, P, P, P, I, I, I, P, SZ, P], I),
+    "fq_gemm_q_workspace_bytes": ([I, I, I], SZ),
+    "fq_gemm_w6ax_q": ([P, P, P, I, I, I, I, P, P, P, I, I, I, P, SZ, P], I),
     "fq_linear_w6ax_gather": ([P, I, I, I, I, P, P, P, P, P, SZ, P], I),
     "fq_gather_wait": ([P, P, P], I),
     "fq_rmsnorm_linear_scratch_bytes": ([I, I, I], SZ),

@@ -351,6 +351,61 @@ __device__ __forceinline__ void decode_splitk_fixup(int nit, int S, int M, int N
     }
 }
 
+// ---- the next linear's codes in the decode GEMM's epilogue (fq_gemm_w6ax_q at M <= 16, S = 1; VERDICT
+// r05 item 2).  A 16-column tile never holds a whole 128-column group, so the group's absmax has to cross
+// workgroups: every workgroup's output pairs go out as agent-scope (sc1) stores; it drains them, takes one
+// agent-scope ticket per 128-column group of its tiles (8 tiles, fewer at the right edge), and the last
+// arriver of a group re-loads the group's M x 128 outputs (sc1 loads) and quantizes them exactly as
+// fq_quantize_act does (quant_group16), reading d's leading qM * qK values as the flat [qM][qK] next input
+// (N % 128 == 0: a 128-column group of d is a group of the next input).  The hand-off rule of
+// decode_splitk_fixup below: nothing polls; the last arriver learns it from its own add, and it resets
+// the ticket for the next launch.
+struct DecodeQ {
+    int8_t *qxq;    // int8 [qM][qK]
+    uint16_t *qxs;  // fp16 [qK / 128][qM]
+    int qM, qK, qbits;
+};
+template <int NW>
+__device__ __forceinline__ void decode_qe_epilogue(int nit, int M, int N, int t0, int tstep, uint32_t *__restrict__ tickets,
+                                                   const uint16_t *__restrict__ d, int *flag, const DecodeQ &qe) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 output stores
+    __syncthreads();
+    const long lim = (long)qe.qM * qe.qK;
+    const int NT = N >> 4;
+    for (int it = threadIdx.x; it < nit; it += NW * 64) {
+        const int q = (t0 + it * tstep) >> 3;
+        int last = 0;
+        if ((long)q * FQ_GROUP < lim) {  // (row 0 of the group is part of the next input)
+            const int nt = NT - 8 * q < 8 ? NT - 8 * q : 8;
+            const uint32_t prev = __hip_atomic_fetch_add(&tickets[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = prev == (uint32_t)(nt - 1);
+            if (last) __hip_atomic_store(&tickets[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        flag[it] = last;
+    }
+    __syncthreads();  // (the flags are read behind this barrier: the re-loads cannot move above it)
+    const int pr = threadIdx.x >> 4, qsub = threadIdx.x & 15;  // 16 lanes per (row, group), 8 values each
+    for (int it = 0; it < nit; it++) {
+        if (!flag[it]) continue;  // workgroup-uniform
+        const int q = (t0 + it * tstep) >> 3;
+        for (int row = pr; row < M; row += NW * 4) {
+            const long f0 = (long)row * N + (long)q * FQ_GROUP;  // the group's flat index
+            if (f0 >= lim) continue;  // (uniform over the row's 16 lanes, as quant_group16's DPP needs)
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(d + f0 + qsub * 8);
+            const uint64_t a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t b = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint2 codes;
+            const uint16_t sh = quant_group16(make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)),
+                                              qe.qbits, codes);
+            *reinterpret_cast<uint2 *>(qe.qxq + f0 + qsub * 8) = codes;
+            if (qsub == 0) {
+                const long r2 = f0 / qe.qK;
+                qe.qxs[(f0 - r2 * qe.qK) / FQ_GROUP * qe.qM + r2] = sh;
+            }
+        }
+    }
+}
+
 // Producer fused into the FUSE prologue (fq_rmsnorm_linear_w6ax / fq_silu_linear_w6ax):
 //   PRO = 1: xh is the residual; r = half_clamp(in + residual) when `in`, RMSNorm with gamma, then
 //            the quantizer (M = 1, K = 4 * 128 * NW, S = 1: wave w's four groups are exactly the
@@ -480,12 +535,12 @@ __device__ __forceinline__ void chain_ring_ahead(uint32_t nxt_w, uint32_t nxt_p)
 // group quantizer (quant_group16, bit-identical to fq_quantize_act) over its own groups straight
 // into the staged LDS regions, so a decode linear is one launch.  Requires XS = SS = 0.
 template <int MT, int XS, int SS, bool FUSE, bool DBG, int ABL = 0, bool CH = false, int PRO = 0, bool GAT = false,
-          bool CHN = false, bool CHP = false>
+          bool CHN = false, bool CHP = false, bool QE = false>
 __device__ __forceinline__ void decode_body(
     const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint16_t *__restrict__ xh, int abits,
     const uint32_t *__restrict__ wpk, int Mall, int N, int K, uint16_t *__restrict__ d, int32_t *__restrict__ acc_dbg,
     float *__restrict__ slabs, uint32_t *__restrict__ tickets, int S, int IPW, int RC, int xwin, int iq, int ir,
-    int NCH, const fq_gather *__restrict__ gat, const DecodePro &pro, int gridall = -1) {
+    int NCH, const fq_gather *__restrict__ gat, const DecodePro &pro, int gridall = -1, DecodeQ qe = DecodeQ{}) {
     if (gridall < 0) gridall = (int)gridDim.x;  // (the plain kernel passes it: no hidden-argument load)
     // Every kernel argument is needed before the first DMA: make the compiler load them all in
     // ONE batch here (it would otherwise issue a second s_load batch after the index math, a
@@ -504,6 +559,8 @@ __device__ __forceinline__ void decode_body(
     static_assert(!FUSE || (XS == 0 && SS == 0), "fused quantization stages into LDS");
     static_assert(PRO == 0 || (FUSE && !CH), "fused producers run in the fused quantizer's prologue");
     static_assert(!CHN || (FUSE && PRO == 0 && !GAT && !CH && !DBG), "the chain runs plain fused linears");
+    static_assert(!QE || (!FUSE && PRO == 0 && !GAT && !CH && !DBG && !CHN && MT <= 16),
+                  "the epilogue quantizer runs on the plain unfused decode GEMM");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     FQ_STAMP(0);
     FQ_CSTAMP(0);
@@ -1291,7 +1348,7 @@ __device__ __forceinline__ void decode_body(
             // (k = e / EM by a multiply-high with ceil(2^32 / EM): exact while e * EM < 2^32 -- e < IPW * EM
             // with IPW <= 4096 and EM <= 512 -- instead of a per-element integer division)
             const uint32_t emi = (uint32_t)(0xffffffffu / (uint32_t)EM) + 1u;
-            if ((GAT || CHN) && S == 1) {  // peer-store gather / chain: two adjacent columns per thread
+            if ((GAT || CHN || QE) && S == 1) {  // peer-store gather / chain / QE: two adjacent columns per thread
                 for (int e = 2 * threadIdx.x; e < (rs + 1) * EM; e += 2 * NW * 64) {
                     const int k = (int)(((uint64_t)(uint32_t)e * emi) >> 32), ee = e - k * EM;
                     float v0 = 0.f, v1 = 0.f;
@@ -1300,7 +1357,11 @@ __device__ __forceinline__ void decode_body(
                         v0 += red[(k * NW + w) * EM + ee];
                         v1 += red[(k * NW + w) * EM + ee + 1];
                     }
-                    if (CHN)
+                    if (QE)  // (sc1: the group's last arriver re-loads it; N % 128 == 0, so the pair is in range)
+                        __hip_atomic_store(reinterpret_cast<uint32_t *>(d + (long)(ee >> 4) * N + 16 * item_tile(it - rs + k) + (ee & 15)),
+                                           (uint32_t)f2h(v0) | ((uint32_t)f2h(v1) << 16), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    else if (CHN)
                         chain_store2(d, pro.hd, otag, N, ee >> 4,
                                      16 * item_tile(it - rs + k) + (ee & 15), v0, v1);
                     else
@@ -1328,6 +1389,10 @@ __device__ __forceinline__ void decode_body(
     }
     FQ_STAMP(3);
     FQ_CSTAMP(4);
+    if constexpr (QE) {  // (S = 1)
+        decode_qe_epilogue<NW>(nit, M, N, t0, tstep, tickets, d, flag, qe);
+        return;
+    }
     if constexpr (CHN) {  // (S = 1)
         if (eupd) chain_epoch_update(pro.chain, chain_late(pro.epoch), eseen, gridall);
         // the next linear's prologue reuses the LDS: every wave is past this one's
@@ -1399,6 +1464,21 @@ __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_kernel(
         FUSE ? nullptr : reinterpret_cast<const int8_t *>(x), xs, FUSE ? reinterpret_cast<const uint16_t *>(x) : nullptr,
         abits, wpk, Mall, N, K, d, nullptr, reinterpret_cast<float *>(ws + FQ_TICKET_BYTES),
         reinterpret_cast<uint32_t *>(ws), S, IPW, RC, xwin, iq, ir, NCH, nullptr, DecodePro{}, grid);
+}
+// The plain kernel with the next linear's codes in its epilogue (decode_qe_epilogue): the same preloaded
+// fields, then the quantizer's outputs (needed only at the end, read from kernarg memory).
+template <int MT, int XS, int SS>
+__global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_q_kernel(
+    const int8_t *__restrict__ xq, const uint16_t *__restrict__ xs, const uint32_t *__restrict__ wpk,
+    uint16_t *__restrict__ d, char *__restrict__ ws, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+    int8_t *__restrict__ qxq, uint16_t *__restrict__ qxs, int qM, int qK, int qbits) {
+    const int N = w0 & 0x1fffff, abits = (w0 >> 21) & 15, xwin = w0 >> 25;
+    const int K = (w1 & 0x1fff) * FQ_GROUP;
+    const int IPW = w2 & 0xffff, RC = w2 >> 16;
+    const int Mall = w3 & 1023, ir = (w3 >> 10) & 2047, grid = w3 >> 21;
+    decode_body<MT, XS, SS, false, false, 0, false, 0, false, false, false, true>(
+        xq, xs, nullptr, abits, wpk, Mall, N, K, d, nullptr, nullptr, reinterpret_cast<uint32_t *>(ws), 1, IPW, RC,
+        xwin, IPW - (ir != 0), ir, 1, nullptr, DecodePro{}, grid, DecodeQ{qxq, qxs, qM, qK, qbits});
 }
 template <int MT, int XS, int SS, bool FUSE, bool CH>
 __global__ __launch_bounds__(decode_waves(MT) * 64) void fq_gemm_decode_dbg_kernel(FQ_DECODE_ARGS) {
@@ -3391,20 +3471,98 @@ extern "C" fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const
     return launch_prefill_u8(xq, xs, w_packed, (const char *)w_u8, M, N, K, d, acc_dbg, (hipStream_t)stream);
 }
 
-extern "C" fq_status fq_gemm_w6ax_u8_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8,
-                                       int M, int N, int K, int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM,
-                                       int qK, int qbits, void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+// The next input's arguments of fq_gemm_w6ax_q / _u8_q: its buffers are written while other workgroups
+// still read the operands, so nothing may overlap.
+static fq_status q_args_check(const int8_t *xq, const uint16_t *xs, int M, int N, int K, const uint16_t *d,
+                              const int8_t *qxq, const uint16_t *qxs, int qM, int qK, int qbits) {
     if (!qxq || !qxs) return FQ_ERR_NULL;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP) return FQ_ERR_SHAPE;
     if (qM <= 0 || qK <= 0 || qK % FQ_GROUP || (size_t)qM * qK > (size_t)M * N) return FQ_ERR_SHAPE;
     if (qbits != 6 && qbits != 8) return FQ_ERR_BITS;
-    // the next input's buffers are written while other workgroups still read the operands: no overlap
     const size_t qb = (size_t)qM * qK, qsb = (size_t)(qK / FQ_GROUP) * qM * 2, db = (size_t)M * N * 2;
     if (ranges_overlap(qxq, qb, xq, (size_t)M * K) || ranges_overlap(qxq, qb, xs, (size_t)(K / FQ_GROUP) * M * 2) ||
         ranges_overlap(qxq, qb, d, db) || ranges_overlap(qxs, qsb, xq, (size_t)M * K) ||
         ranges_overlap(qxs, qsb, xs, (size_t)(K / FQ_GROUP) * M * 2) || ranges_overlap(qxs, qsb, d, db) ||
         ranges_overlap(qxq, qb, qxs, qsb))
         return FQ_ERR_SHAPE;
-    if (M < PF_U8_MIN_M || N % FQ_GROUP) {  // (no epilogue form: the GEMM, then the quantizer -- the same bits)
+    return FQ_OK;
+}
+
+// Decode sizes with the quantizer in the GEMM's epilogue (decode_qe_epilogue): the unfused plan at
+// M <= 16 with no k-split and one ticket per 128-column group of d.
+static bool decode_q_plan(int M, int N, int K, DecodePlan *p) {
+    if (M > 16 || N % FQ_GROUP || (size_t)(N / FQ_GROUP) > kTicketBytes / 4 || (size_t)M * N >= ((size_t)1 << 31))
+        return false;
+    *p = decode_plan(M, N, K, false);
+    return p->fits && p->S == 1 && p->NCH == 1 && p->MT <= 16;
+}
+template <int MT, int XS, int SS>
+static fq_status launch_decode_q(const DecodePlan &p, const int8_t *xq, const uint16_t *xs, const void *wpk, int M,
+                                 int N, int K, int abits, uint16_t *d, void *ws, const DecodeQ &q, hipStream_t s) {
+    if ((size_t)p.NT * (K / FQ_GROUP) * FQ_BLOCK >= ((size_t)1 << 32)) return FQ_ERR_SHAPE;  // (buffer offsets)
+    DecodePacked pk;
+    if (p.NT / p.grid != p.IPW - (p.NT % p.grid != 0) ||
+        !decode_pack(N, K, abits, p.xwin, 1, 1, p.IPW, p.RC, M, p.NT % p.grid, p.grid, &pk))
+        return FQ_ERR_SHAPE;
+    hipLaunchKernelGGL((fq_gemm_decode_q_kernel<MT, XS, SS>), dim3(p.grid), dim3(decode_waves(MT) * 64),
+                       decode_lds_bytes(p, M, N, K), s, xq, xs, (const uint32_t *)wpk, d, (char *)ws, pk.w0, pk.w1,
+                       pk.w2, pk.w3, q.qxq, q.qxs, q.qM, q.qK, q.qbits);
+    FQ_LAUNCH_CHECK();
+    return FQ_OK;
+}
+template <int MT>
+static fq_status dispatch_decode_q(const DecodePlan &p, const int8_t *xq, const uint16_t *xs, const void *wpk, int M,
+                                   int N, int K, int abits, uint16_t *d, void *ws, const DecodeQ &q, hipStream_t s) {
+    if (p.XS == 0) return launch_decode_q<MT, 0, 0>(p, xq, xs, wpk, M, N, K, abits, d, ws, q, s);
+    if (p.SS == 0) return launch_decode_q<MT, 1, 0>(p, xq, xs, wpk, M, N, K, abits, d, ws, q, s);
+    return launch_decode_q<MT, 1, 1>(p, xq, xs, wpk, M, N, K, abits, d, ws, q, s);
+}
+
+extern "C" size_t fq_gemm_q_workspace_bytes(int M, int N, int K) {
+    const size_t g = fq_gemm_workspace_bytes(M, N, K);
+    DecodePlan p;
+    if (M <= 0 || N <= 0 || K <= 0 || K % FQ_GROUP || !decode_q_plan(M, N, K, &p)) return g;
+    return g > kTicketBytes ? g : kTicketBytes;  // (the epilogue's group tickets)
+}
+
+extern "C" fq_status fq_gemm_w6ax_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
+                                    int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM, int qK, int qbits,
+                                    void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+    if (!xq || !xs || !w_packed || !d) return FQ_ERR_NULL;
+    const fq_status qs = q_args_check(xq, xs, M, N, K, d, qxq, qxs, qM, qK, qbits);
+    if (qs != FQ_OK) return qs;
+    if (abits != 6 && abits != 8) return FQ_ERR_BITS;
+    DecodePlan p;
+#ifdef FQ_DEV_ABLATION
+    const bool noq = getenv("FQ_DEV_NOQE") && atoi(getenv("FQ_DEV_NOQE"));  // (development: the two-launch form)
+#else
+    const bool noq = false;
+#endif
+    if (!noq && decode_q_plan(M, N, K, &p) && workspace && workspace_bytes >= kTicketBytes) {
+        const DecodeQ q = {qxq, qxs, qM, qK, qbits};
+        hipStream_t s = (hipStream_t)stream;
+        switch (p.MT) {
+            case 4: return dispatch_decode_q<4>(p, xq, xs, w_packed, M, N, K, abits, d, workspace, q, s);
+            case 8: return dispatch_decode_q<8>(p, xq, xs, w_packed, M, N, K, abits, d, workspace, q, s);
+            default: return dispatch_decode_q<16>(p, xq, xs, w_packed, M, N, K, abits, d, workspace, q, s);
+        }
+    }
+    // (no epilogue form, or no ticket workspace: the GEMM, then the quantizer -- the same bits)
+    const fq_status st = fq_gemm_w6ax(xq, xs, w_packed, M, N, K, abits, d, nullptr, workspace, workspace_bytes, stream);
+    return st != FQ_OK ? st : fq_quantize_act(d, qM, qK, qbits, qxq, qxs, stream);
+}
+
+extern "C" fq_status fq_gemm_w6ax_u8_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8,
+                                       int M, int N, int K, int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM,
+                                       int qK, int qbits, void *workspace, size_t workspace_bytes, fq_stream_t stream) {
+    const fq_status qs = q_args_check(xq, xs, M, N, K, d, qxq, qxs, qM, qK, qbits);
+    if (qs != FQ_OK) return qs;
+    if (M < PF_U8_MIN_M) {  // (decode and mid-M plans do not read the unpacked operands: fq_gemm_w6ax_q's forms)
+        if (!w_u8) return FQ_ERR_NULL;
+        return fq_gemm_w6ax_q(xq, xs, w_packed, M, N, K, abits, d, qxq, qxs, qM, qK, qbits, workspace, workspace_bytes,
+                              stream);
+    }
+    if (N % FQ_GROUP) {  // (no epilogue form: the GEMM, then the quantizer -- the same bits)
         const fq_status st = fq_gemm_w6ax_u8(xq, xs, w_packed, w_u8, M, N, K, abits, d, nullptr, workspace,
                                              workspace_bytes, stream);
         return st != FQ_OK ? st : fq_quantize_act(d, qM, qK, qbits, qxq, qxs, stream);

@@ -235,11 +235,18 @@ def gemm_w6ax(xq, xs, wpk, N, abits=6, return_acc=False, out=None, w_u8=None):
     return (out, acc) if return_acc else out
 
 
+def gemm_q_workspace_bytes(M, N, K):
+    """Workspace of gemm_w6ax_q's one-launch form (fq_gemm_q_workspace_bytes): the GEMM's own plus the
+    epilogue quantizer's group tickets."""
+    return int(_lib.load().fq_gemm_q_workspace_bytes(M, N, K))
+
+
 def gemm_w6ax_q(xq, xs, wpk, N, abits, w_u8, q_shape, qbits, out=None):
-    """gemm_w6ax over prepared operands (w_u8, prefill sizes) that also returns the NEXT linear's
-    quantized input (fq_gemm_w6ax_u8_q): the fp16 output's leading qM * qK values read row-major as
-    [qM, qK] and quantized to qbits -- bit-identical to quantize_act(out.view(-1)[:qM*qK].view(qM, qK),
-    qbits), computed in the 256 x 256 prefill kernel's epilogue.  Returns (out, qxq, qxs)."""
+    """gemm_w6ax that also returns the NEXT linear's quantized input: the fp16 output's leading qM * qK
+    values read row-major as [qM, qK] and quantized to qbits -- bit-identical to
+    quantize_act(out.view(-1)[:qM*qK].view(qM, qK), qbits).  Prefill sizes over prepared operands
+    (w_u8, fq_gemm_w6ax_u8_q): in the 256 x 256 prefill kernel's epilogue; M <= 16 (w_u8 None,
+    fq_gemm_w6ax_q): in the decode GEMM's epilogue, one launch.  Returns (out, qxq, qxs)."""
     _dev(xq, torch.int8, "xq", 2)
     M, K = xq.shape
     _k_ok(K)
@@ -251,9 +258,10 @@ def gemm_w6ax_q(xq, xs, wpk, N, abits, w_u8, q_shape, qbits, out=None):
     _k_ok(qK)
     _need(0 < qM * qK <= M * N, "the next input must be a prefix of the output")
     dev = xq.device
-    _dev(w_u8, torch.uint8, "w_u8", 1)
-    _need(w_u8.numel() >= int(_lib.load().fq_prefill_weight_bytes(N, K)) and w_u8.device == dev,
-          "w_u8 must be prepare_prefill_weights(wpk, N, K) on the operands' device")
+    if w_u8 is not None:
+        _dev(w_u8, torch.uint8, "w_u8", 1)
+        _need(w_u8.numel() >= int(_lib.load().fq_prefill_weight_bytes(N, K)) and w_u8.device == dev,
+              "w_u8 must be prepare_prefill_weights(wpk, N, K) on the operands' device")
     if out is None:
         out = torch.empty((M, N), dtype=torch.float16, device=dev)
     else:
@@ -262,10 +270,15 @@ def gemm_w6ax_q(xq, xs, wpk, N, abits, w_u8, q_shape, qbits, out=None):
     qxq = torch.empty((qM, qK), dtype=torch.int8, device=dev)
     qxs = torch.empty((qK // GROUP, qM), dtype=torch.float16, device=dev)
     s = _stream(xq)
-    nb = gemm_workspace_bytes(M, N, K)
-    wbuf = workspace(dev, nb, s.value)
-    _lib.call("fq_gemm_w6ax_u8_q", _ptr(xq), _ptr(xs), _ptr(wpk), _ptr(w_u8), M, N, K, abits, _ptr(out), _ptr(qxq),
-              _ptr(qxs), qM, qK, qbits, _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    if w_u8 is not None:
+        wbuf = workspace(dev, gemm_workspace_bytes(M, N, K), s.value)
+        _lib.call("fq_gemm_w6ax_u8_q", _ptr(xq), _ptr(xs), _ptr(wpk), _ptr(w_u8), M, N, K, abits, _ptr(out),
+                  _ptr(qxq), _ptr(qxs), qM, qK, qbits, _ptr(wbuf),
+                  ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
+    else:
+        wbuf = workspace(dev, gemm_q_workspace_bytes(M, N, K), s.value)
+        _lib.call("fq_gemm_w6ax_q", _ptr(xq), _ptr(xs), _ptr(wpk), M, N, K, abits, _ptr(out), _ptr(qxq), _ptr(qxs),
+                  qM, qK, qbits, _ptr(wbuf), ctypes.c_size_t(wbuf.numel() if wbuf is not None else 0), s)
     return out, qxq, qxs
 
 

@@ -49,9 +49,11 @@ typedef struct ihipStream_t *fq_stream_t; /* == hipStream_t */
  * fq_bmma_init_image) and fq_bmma_state carries w_format / prepared; split-K prefill without its
  * workspace returns FQ_ERR_WORKSPACE.  A caller built against another version should compare
  * FQ_ABI_VERSION with fq_abi_version() at start-up. */
-#define FQ_ABI_VERSION 5   /* 4: FQ_ERR_TIMEOUT and the host-visible chain status (fq_chain_bind_status);
+#define FQ_ABI_VERSION 6   /* 4: FQ_ERR_TIMEOUT and the host-visible chain status (fq_chain_bind_status);
                               5: fq_chain_bind_status takes the chain workspace's size and zeroes the word,
-                                 a timed-out chain writes NaN outputs */
+                                 a timed-out chain writes NaN outputs;
+                              6: fq_gemm_w6ax_q / fq_gemm_q_workspace_bytes (the next input's codes from the
+                                 decode GEMM's epilogue) */
 int fq_abi_version(void);
 
 typedef int fq_status;
@@ -219,6 +221,19 @@ fq_status fq_gemm_w6ax_u8(const int8_t *xq, const uint16_t *xs, const void *w_pa
 fq_status fq_gemm_w6ax_u8_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, const void *w_u8, int M,
                             int N, int K, int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM, int qK,
                             int qbits, void *workspace, size_t workspace_bytes, fq_stream_t stream);
+/* The same at any M without prepared operands: fq_gemm_w6ax, then the next input's codes -- bit-identical
+ * to fq_quantize_act(d, qM, qK, qbits, qxq, qxs) after the GEMM; the same argument rules (FQ_ERR_SHAPE on
+ * an overlap).  At M <= 16 with N % 128 == 0 and no k-split the quantizer runs in the decode GEMM's
+ * epilogue: every workgroup stores its 16-column tiles write-through, takes one agent-scope ticket per
+ * 128-column group, and the group's last workgroup re-loads its M x 128 outputs and quantizes them (one
+ * launch instead of two; the reference quantizes every input in its own packing kernel,
+ * flexq_gemm_wrapper.cu:99-122).  That form needs a workspace of fq_gemm_q_workspace_bytes(M, N, K)
+ * bytes, initialised once by fq_workspace_init (its tickets return to zero after every launch); with a
+ * shorter one the call runs the two-launch form (same bits).  fq_gemm_w6ax_u8_q below M = 2048 is this. */
+size_t fq_gemm_q_workspace_bytes(int M, int N, int K);
+fq_status fq_gemm_w6ax_q(const int8_t *xq, const uint16_t *xs, const void *w_packed, int M, int N, int K,
+                         int abits, uint16_t *d, int8_t *qxq, uint16_t *qxs, int qM, int qK, int qbits,
+                         void *workspace, size_t workspace_bytes, fq_stream_t stream);
 
 /* ---- fused producers of the activation codes ---------------------------- */
 /* Residual add + RMSNorm (T5 / LLaMA style: no mean, no bias) + dynamic group quantization, one

@@ -171,3 +171,31 @@ def test_prefill_quantized_output_host_checks():
     assert call(qx, qs, M, K, 7) == 3
     assert call(xq, qs, M, K, 8) == 2              # codes over the operand codes
     assert call(qx, P(5 << 32), M, K, 8) == 2      # scales over the output
+
+
+def test_decode_quantized_output_host_checks():
+    """fq_gemm_w6ax_q (the next input's codes from the decode GEMM's epilogue): the same host-side
+    validation as fq_gemm_w6ax_u8_q before any device call, and its workspace -- the group tickets on
+    top of the GEMM's own -- only where the one-launch form runs (M <= 16, N % 128 == 0, no k-split)."""
+    from flexq_amd import _lib
+    lib = _lib.load()
+    P = ctypes.c_void_p
+    M, N, K = 16, 4096, 4096
+    xq, xs, w, d = P(1 << 32), P(2 << 32), P(3 << 32), P(5 << 32)
+    qx, qs = P(6 << 32), P(7 << 32)
+    call = lambda qxq, qxs, qM, qK, qb, ab=6: lib.fq_gemm_w6ax_q(xq, xs, w, M, N, K, ab, d, qxq, qxs, qM, qK, qb,  # noqa: E731
+                                                                   None, 0, None)
+    assert lib.fq_gemm_w6ax_q(None, xs, w, M, N, K, 6, d, qx, qs, M, K, 6, None, 0, None) == 1
+    assert call(None, qs, M, K, 6) == 1
+    assert call(qx, qs, M, 100, 6) == 2
+    assert call(qx, qs, 2 * M, N, 6) == 2           # more than the output holds
+    assert call(qx, qs, M, K, 7) == 3
+    assert call(qx, qs, M, K, 6, ab=5) == 3
+    assert call(xq, qs, M, K, 6) == 2               # codes over the operand codes
+    assert call(qx, P(5 << 32), M, K, 6) == 2       # scales over the output
+    tickets = lib.fq_gemm_q_workspace_bytes(1, 12288, 4096)
+    assert tickets >= 4 * (12288 // 128) and lib.fq_gemm_workspace_bytes(1, 12288, 4096) == 0
+    assert lib.fq_gemm_q_workspace_bytes(16, 22016, 4096) == tickets
+    assert lib.fq_gemm_q_workspace_bytes(17, 4096, 4096) == lib.fq_gemm_workspace_bytes(17, 4096, 4096)
+    assert lib.fq_gemm_q_workspace_bytes(16, 4112, 4096) == lib.fq_gemm_workspace_bytes(16, 4112, 4096)
+    assert lib.fq_gemm_q_workspace_bytes(16, 4096, 100) == 0

@@ -818,3 +818,77 @@ def test_prefill_split_k_without_workspace_is_an_error(ops, dev):
     rc = L.fq_gemm_w6ax(P(xq.data_ptr()), P(xs.data_ptr()), P(pk.data_ptr()), M, N, K, 8, P(d.data_ptr()), None,
                         None, 0, None)
     assert rc == 4  # FQ_ERR_WORKSPACE
+
+
+# fq_gemm_w6ax_q at decode sizes: the next linear's codes from the decode GEMM's epilogue (group tickets,
+# the last workgroup of each 128-column group quantizes it).  C3's four hand-offs (down's A8 input a prefix
+# whose rows straddle gate_up's), M = 1 / 4 / 8 / ragged 13, and two shapes that take the two-launch form
+# (N % 128 != 0; a k-split plan).
+@pytest.mark.parametrize("M,N,K,qM,qK,qbits", [
+    (16, 12288, 4096, 16, 4096, 6),    # qkv -> o: the output's leading third
+    (16, 4096, 4096, 16, 4096, 6),     # o -> gate_up
+    (16, 22016, 4096, 16, 11008, 8),   # gate_up -> down (A8)
+    (16, 4096, 11008, 16, 4096, 6),    # down -> the next layer's qkv
+    (1, 12288, 4096, 1, 4096, 6),
+    (4, 4096, 4096, 4, 4096, 8),
+    (8, 4224, 4096, 8, 4224, 6),       # 33 groups, 264 tiles: two items on 8 workgroups
+    (13, 4096, 4096, 13, 4096, 6),     # ragged rows in the 16-row tile
+    (16, 4112, 4096, 16, 4096, 6),     # N % 128 != 0: the GEMM, then the quantizer
+    (16, 1024, 4096, 16, 1024, 6),     # narrow N: a k-split plan, the two-launch form
+])
+def test_decode_quantized_output_bit_identical(ops, dev, M, N, K, qM, qK, qbits):
+    """fq_gemm_w6ax_q: codes and scales bit-identical to fq_quantize_act over the fp16 output's leading
+    qM x qK values, the output the plain GEMM's, and the same again on a second call and on graph
+    replays (the group tickets return to zero after every launch)."""
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N + qK)
+    xq = torch.randint(-32, 32, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    d0 = ops.gemm_w6ax(xq, xs, pk, N, 6)
+    rq, rs = ops.quantize_act(d0.view(-1)[:qM * qK].view(qM, qK), qbits)
+    for _ in range(2):
+        d1, qxq, qxs = ops.gemm_w6ax_q(xq, xs, pk, N, 6, None, (qM, qK), qbits)
+        torch.cuda.synchronize()
+        assert torch.equal(d0.view(torch.int16), d1.view(torch.int16))
+        assert torch.equal(qxs.view(torch.int16), rs.view(torch.int16))
+        assert torch.equal(qxq, rq)
+    s = torch.cuda.Stream(dev)
+    d2 = torch.empty_like(d0)
+    with torch.cuda.stream(s):
+        ops.gemm_w6ax_q(xq, xs, pk, N, 6, None, (qM, qK), qbits, out=d2)  # (sizes the stream's workspace)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        _, gq, gs = ops.gemm_w6ax_q(xq, xs, pk, N, 6, None, (qM, qK), qbits, out=d2)
+    for _ in range(3):
+        gq.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(gq, rq) and torch.equal(gs.view(torch.int16), rs.view(torch.int16))
+
+
+def test_c3_epilogue_quantized_codes_against_the_oracle(ops, dev):
+    """C3's gate_up -> down hand-off in the decode epilogue form (M = 16, the next input [16, 11008] A8 is
+    the output's leading values, its rows straddling gate_up's): the codes and scales bit-exact against
+    the oracle's engine quantizer applied to the GEMM's own fp16 output, and that output within the
+    oracle's GEMM tolerance."""
+    M, N, K, qM, qK = 16, 22016, 4096, 16, 11008
+    g = torch.Generator(device=dev).manual_seed(37)
+    xq = torch.randint(-32, 32, (M, K), dtype=torch.int8, device=dev, generator=g)
+    wq = torch.randint(-32, 32, (N, K), dtype=torch.int8, device=dev, generator=g)
+    xs = (torch.rand((K // 128, M), device=dev, generator=g) * 0.05).half()
+    ws = (torch.rand((K // 128, N), device=dev, generator=g) * 0.05).half()
+    pk = ops.pack_w6(wq, ws)
+    d, qxq, qxs = ops.gemm_w6ax_q(xq, xs, pk, N, 6, None, (qM, qK), 8)
+    torch.cuda.synchronize()
+    q_ref, s_ref = oracle.quantize_engine(host(d.view(-1)[:qM * qK].view(qM, qK)), 8)
+    np.testing.assert_array_equal(host(qxq), q_ref)
+    np.testing.assert_array_equal(host(qxs).view(np.uint16), s_ref.view(np.uint16))
+    r = rng(13)
+    cols = np.sort(np.concatenate([r.choice(N, size=126, replace=False), [0, N - 1]]))
+    cols_t = torch.from_numpy(cols).to(dev)
+    ref, _, mag = oracle.gemm(host(xq), np.ascontiguousarray(host(xs)), host(wq.index_select(0, cols_t)),
+                              np.ascontiguousarray(host(ws.index_select(1, cols_t))))
+    assert_gemm_close(host(d.index_select(1, cols_t)), ref, mag, "C3 gate_up (epilogue form)")
