@@ -2612,12 +2612,14 @@ static DecodePlan decode_plan(int M, int N, int K, bool fused, int pro = 0) {
     // (fused: the fully staged variant with the largest fp16 window that fits)
     const int modes[3][2] = {{0, 0}, {1, 0}, {1, 1}};
     const int nm = fused ? 1 : 3;
-    // One item per workgroup at 16 rows: the activation rows ride in the ring slots (XS = 1) -- the same
-    // bytes as the up-front staging, but no 8-instruction LDS-DMA burst before the first block: 4096 x
-    // 4096 5.17 vs 5.74 us per launch; with more items the rows would be fetched once per item (12288 x
-    // 4096, 3 items: 9.88 vs 9.56; 22016: 18.0 vs 15.4; profiles/r06_m16_xs_ab.txt).  Same bits: XS moves
-    // the rows, not the summation.
-    int m0 = !fused && p.MT == 16 && p.IPW == 1 ? 1 : 0;
+    // One item per workgroup at 5-16 rows: the activation rows ride in the ring slots (XS = 1) -- the
+    // same bytes as the up-front staging, but no LDS-DMA burst before the first block (M = 16, 4096 x
+    // 4096: 5.17 vs 5.74 us per launch; M = 8: 4.88 vs 5.29, 4096 x 11008 8.75 vs 9.67).  Not with more
+    // items (the rows would be fetched once per item: M = 16, 12288 x 4096, 3 items 9.88 vs 9.56; 22016
+    // 18.0 vs 15.4), nor for 16-row tiles over long K, whose slots carry 16 rows whatever M (M = 12, 4096 x
+    // 11008: 9.7 vs 9.0).  profiles/r06_m16_xs_ab.txt, r06_m8_xs_ab.txt.  Same bits: XS moves the rows, not
+    // the summation.
+    int m0 = !fused && p.IPW == 1 && (p.MT == 8 || (p.MT == 16 && K <= 8192)) ? 1 : 0;
 #ifdef FQ_DEV_ABLATION
     if (const char *e = getenv("FQ_DEV_XS"); e && !fused) m0 = atoi(e) == 1 ? 1 : 0;  // development: force either
 #endif
