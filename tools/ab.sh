@@ -16,6 +16,9 @@
 # AB_TESTS="tests/test_gpu_chain.py ..."  runs those GPU tests against EVERY library first and stops on a
 #   failure (an A/B of a variant that is not bit-identical is not an A/B); AB_TESTS_K="expr" selects with
 #   pytest -k (leave out tests of the behaviour the variant changes); AB_OUT=file tees the table.
+# AB_ENVS="FQ_DEV_XS=0 FQ_DEV_XS=1" makes each environment setting an arm of its own with every library
+#   (development switches read at run time, e.g. the ablation library's FQ_DEV_*; "-" = no setting;
+#   comma-separate several variables of one arm).
 # One gpurun call per experiment:  AB_TESTS=... bash tools/ab.sh step 3 flexq_amd/libflexq_hip.so abtmp/x.so
 set -o pipefail
 MODE=$1; REPS=$2; shift 2
@@ -32,8 +35,9 @@ fi
 B="python3 -u bench.py --cpu-budget 0 --no-fp16-compare --no-calibrate"
 J='import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1])'
 for rep in $(seq "$REPS"); do
-  for L in "$@"; do
-    printf "%s " "$L"
+  for L in "$@"; do for E in ${AB_ENVS:--}; do
+    printf "%s " "$L"; [ "$E" != - ] && printf "%s " "$E"
+    ( [ "$E" != - ] && export ${E//,/ }
     case $MODE in
       step)    FLEXQ_AMD_LIB=$L timeout -k 10 200 $B --no-layers --no-extra-configs 2>/dev/null |
                  python3 -c "$J; print(d['ms_per_step'], d['roofline']['per_launch_us'])" || exit 1 ;;
@@ -46,6 +50,6 @@ for rep in $(seq "$REPS"); do
       prefill) echo; FQ_REPS=${FQ_REPS:-6} FQ_LIB=$L timeout -k 10 200 python3 tools/prefill_bench.py ${PF_M:-16384} 2>&1 |
                  grep -E "^M=" | sed -E 's/\| linear.*//' || exit 1 ;;
       *) echo "unknown mode $MODE"; exit 2 ;;
-    esac
-  done
+    esac ) || exit 1
+  done; done
 done
