@@ -221,8 +221,9 @@ __device__ __forceinline__ void gather_poll(const fq_gather *__restrict__ g, uin
 // with a fan-in whose last workgroup zeroes the hand-off region and the epoch (tags never repeat
 // over a granule's lifetime, and never have bit 31 set).  Bounded: a wait that does not end within
 // ~1 s sets the error word and goes on; with the error word set later waits return at once.  A linear
-// whose wait failed writes fp16 NaN outputs and tags its granules with bit 31 set (poisoned): its
-// consumers stop waiting on them and fail in turn, so every output downstream of a failure is NaN
+// whose wait failed writes fp16 NaN outputs (its granules carry them); every workgroup that waited on
+// the missing input timed out with it and set the sticky word, which the next linear reads as it
+// starts, so it fails at once and writes NaN in turn: every output downstream of a failure is NaN
 // (results are never undefined-but-plausible) at no cost to the normal path.
 constexpr int FQ_CHAIN_MAX = 8;
 constexpr size_t FQ_CHAIN_SYNC_BYTES = 4096;       // chain workspace: sync words, then the hand-offs
@@ -1002,7 +1003,7 @@ __device__ __forceinline__ void decode_body(
             bool dx = !gr, din = !gin;
             for (int spin = 0; spin < (1 << 20); spin++) {
                 // every load of the pass in flight at once, then the tag compares (a short-circuit &&
-                // between them serialises one round trip per load pair); poisoned tags as the plain chain's
+                // between them serialises one round trip per load pair)
                 uint4 gx0[4], gx1[4], gi0[4], gi1[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
