@@ -155,3 +155,21 @@ def test_multi_gpu_line_is_like_for_like():
     # last resort (a line that would not fit even without the optional sections) keeps them too
     tiny = bench.compact_line(res, None, limit=10)
     assert "same_workload_1gpu" in tiny and "comm" in tiny
+
+
+def test_round6_detail_file_folds_into_the_driver_line():
+    """Round 6's full N = 1 result (the detail file of the final check: C3 with both quantize forms timed,
+    C5 and C4 with theirs, the decoder layers, the reference sweep's per-shape rows) folds into a line
+    under the limit with every essential key and the C3 epilogue-form record kept."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, "profiles", "r06c_bench_detail.json")) as f:
+        res = json.load(f)
+    line = bench.compact_line(res, "d.json")
+    assert len(json.dumps(line)) < 6000
+    for k in bench.ESSENTIAL:
+        assert k in line, k
+    eq = line["c3_llama2_7b_m16"]["epilogue_quantize"]
+    assert eq["last_output_identical"] and "taken" not in eq  # (slower in a graph: not taken)
+    assert line["roofline"]["traffic_source"].startswith("profiles/r06")
