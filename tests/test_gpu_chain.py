@@ -278,8 +278,10 @@ def test_chain_host_status_raises_until_reset(ops, dev):
 
 
 def test_chain_not_coresident_times_out_and_recovers(ops, dev):
-    """The co-residency failure: a kernel on another stream holds half of the CUs for 2.5 s
-    while a chain launches, so half of the chain's workgroups cannot start.  The resident ones' waits end
+    """The co-residency failure: a kernel on another stream holds half of the CUs for 6 s
+    while a chain launches, so half of the chain's workgroups cannot start.  (The blocker must outlast
+    every resident wave's bounded wait, 2^20 polls = 1-2.5 s: a wave still polling when the blocker ends
+    sees the late workgroups' outputs arrive and computes the right values instead of NaN.)  The resident ones' waits end
     after ~1 s with the error word set (never a hang); the kernel itself writes the bound host word and NaN
     over every output that depended on the failed waits, the next call raises ChainTimeoutError, and after
     chain_reset the chain is bit-exact again."""
@@ -300,7 +302,7 @@ def test_chain_not_coresident_times_out_and_recovers(ops, dev):
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     sink = torch.zeros(cus, dtype=torch.int32, device=dev)
     side = torch.cuda.Stream(dev)
-    assert blk.fq_test_cu_blocker(cus // 2, 2500, ctypes.c_void_p(sink.data_ptr()),
+    assert blk.fq_test_cu_blocker(cus // 2, 6000, ctypes.c_void_p(sink.data_ptr()),
                                   ctypes.c_void_p(side.cuda_stream)) == 0
     time.sleep(0.2)  # the blocker is resident
     t0 = time.time()
